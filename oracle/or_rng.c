@@ -1,0 +1,146 @@
+/*
+ * or_rng.c -- TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *
+ * Restatement of the third-party arithmetic behind every reference deal: numpy's legacy RandomState
+ * (MT19937; numpy 2.2.6 in the survey container, reference setup.py:40-43 requires numpy>=1.16.3; the legacy stream is
+ * frozen by numpy's compatibility policy). Published algorithm (Matsumoto & Nishimura mt19937ar.c, as vendored by
+ * numpy's randomkit): init_genrand / init_by_array / genrand_int32 + tempering; numpy's random_interval (masked
+ * rejection) used by RandomState.shuffle (Fisher-Yates, i = n-1 .. 1) and by randint(0, n) / choice(n).
+ * Call sites in the reference: limitholdem/dealer.py:12 (shuffle), leducholdem/game.py:70 and limitholdem/game.py:75
+ * (randint), blackjack/dealer.py:23,32 (shuffle, choice), doudizhu/dealer.py:26 (shuffle).
+ * Pinned by tests/golden/mt19937.npz (seeded by rlcard/utils/seeding.py:33-113) and the canonical mt19937ar vector.
+ */
+#include "oracle.h"
+
+#define MT_N 624
+#define MT_M 397
+
+void or_mt_seed_int(or_mt *s, uint32_t seed)
+{
+    s->key[0] = seed;
+    for (int i = 1; i < MT_N; i++)
+        s->key[i] = 1812433253u * (s->key[i - 1] ^ (s->key[i - 1] >> 30)) + (uint32_t)i;
+    s->pos = MT_N;
+    s->ndraw = 0;
+}
+
+void or_mt_seed_by_array(or_mt *s, const uint32_t *init_key, int key_length)
+{
+    uint32_t *mt = s->key;
+    or_mt_seed_int(s, 19650218u);
+    int i = 1, j = 0;
+    int k = MT_N > key_length ? MT_N : key_length;
+    for (; k; k--) {
+        mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1664525u)) + init_key[j] + (uint32_t)j;
+        i++;
+        j++;
+        if (i >= MT_N) { mt[0] = mt[MT_N - 1]; i = 1; }
+        if (j >= key_length) j = 0;
+    }
+    for (k = MT_N - 1; k; k--) {
+        mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
+        i++;
+        if (i >= MT_N) { mt[0] = mt[MT_N - 1]; i = 1; }
+    }
+    mt[0] = 0x80000000u;
+    s->pos = MT_N;
+    s->ndraw = 0;
+}
+
+static void mt_gen(or_mt *s)
+{
+    uint32_t *mt = s->key, y;
+    int i;
+    for (i = 0; i < MT_N - MT_M; i++) {
+        y = (mt[i] & 0x80000000u) | (mt[i + 1] & 0x7fffffffu);
+        mt[i] = mt[i + MT_M] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+    }
+    for (; i < MT_N - 1; i++) {
+        y = (mt[i] & 0x80000000u) | (mt[i + 1] & 0x7fffffffu);
+        mt[i] = mt[i + (MT_M - MT_N)] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+    }
+    y = (mt[MT_N - 1] & 0x80000000u) | (mt[0] & 0x7fffffffu);
+    mt[MT_N - 1] = mt[MT_M - 1] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+    s->pos = 0;
+}
+
+uint32_t or_mt_next(or_mt *s)
+{
+    if (s->pos == MT_N) mt_gen(s);
+    uint32_t y = s->key[s->pos++];
+    s->ndraw++;
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+uint64_t or_mt_interval(or_mt *s, uint64_t max)
+{
+    if (max == 0) return 0;
+    uint64_t mask = max;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16; mask |= mask >> 32;
+    uint64_t v;
+    /* every range in this path is far below 2^32: numpy takes the 32-bit branch */
+    while ((v = (or_mt_next(s) & mask)) > max) {}
+    return v;
+}
+
+void or_mt_fill(const uint32_t *key, int key_len, uint32_t *out, int n)
+{
+    or_mt s;
+    or_mt_seed_by_array(&s, key, key_len);
+    for (int i = 0; i < n; i++) out[i] = or_mt_next(&s);
+}
+
+void or_mt_shuffle_kat(const uint32_t *key, int key_len, const int *ns, int count, int16_t *out, int stride)
+{
+    or_mt s;
+    or_mt_seed_by_array(&s, key, key_len);
+    for (int c = 0; c < count; c++) {
+        int16_t *x = out + (int64_t)c * stride;
+        for (int i = 0; i < ns[c]; i++) x[i] = (int16_t)i;
+        for (int i = ns[c] - 1; i >= 1; i--) {
+            int j = (int)or_mt_interval(&s, (uint64_t)i);
+            int16_t t = x[i]; x[i] = x[j]; x[j] = t;
+        }
+    }
+}
+
+/* ---- Philox4x32-10 (Salmon et al., SC'11), the policy RNG of cs_rollout ------------------------------------------
+ * counter = (env lo, env hi, t lo, t hi), key = (seed lo, seed hi); the first output word is used. */
+uint32_t or_philox_u32(uint64_t seed, uint64_t env, uint64_t t)
+{
+    uint32_t c0 = (uint32_t)env, c1 = (uint32_t)(env >> 32), c2 = (uint32_t)t, c3 = (uint32_t)(t >> 32);
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    for (int r = 0; r < 10; r++) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n1 = (uint32_t)p1;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        uint32_t n3 = (uint32_t)p0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c0;
+}
+
+/* uniform over the set bits: k = floor(r * count / 2^32), then the k-th set bit in ascending action order */
+int or_policy_pick(uint64_t seed, uint64_t env, uint64_t t, const uint8_t *legal_bits, int num_actions)
+{
+    int count = 0;
+    for (int a = 0; a < num_actions; a++) count += (legal_bits[a >> 3] >> (a & 7)) & 1;
+    if (count == 0) return -1;
+    uint32_t r = or_philox_u32(seed, env, t);
+    int k = (int)(((uint64_t)r * (uint64_t)count) >> 32);
+    for (int a = 0; a < num_actions; a++) {
+        if ((legal_bits[a >> 3] >> (a & 7)) & 1) {
+            if (k == 0) return a;
+            k--;
+        }
+    }
+    return -1;
+}

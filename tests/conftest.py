@@ -1,0 +1,21 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, 'tests')):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs a real MI355X (runs through the HIP engine via the C-ABI)')
+    config.addinivalue_line('markers', 'slow: longer CPU test')
+
+
+@pytest.fixture(scope='session')
+def oracle():
+    import oracle_lib
+    oracle_lib.build()
+    return oracle_lib

@@ -1,0 +1,431 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE (pmcgannon22/rlcard).
+
+Test infrastructure only. This script runs in the build container, where /root/reference exists; it never runs on
+the GPU box and nothing in the product imports it. It copies the reference package into a writable temporary
+directory (``rlcard/games/doudizhu/utils.py:14-19`` extracts ``jsondata.zip`` into the package dir on first import),
+stubs ``termcolor`` (imported eagerly via ``rlcard/envs/__init__.py`` -> uno) and ``typing.Self`` (Python >= 3.11,
+imported by the fork's scout game), then drives the reference ``Env`` objects and records inputs and outputs as
+plain numpy arrays (.npz, loaded with allow_pickle=False).
+
+Fixtures written:
+  mt19937.npz      seed -> init_by_array key (rlcard/utils/seeding.py:33-113), first raw u32 outputs,
+                   shuffle / randint KATs of numpy's legacy RandomState (the RNG behind every deal).
+  leduc.npz        per-seed game streams: reset/step events with the action id fed in (including illegal ids,
+                   to pin _decode_action's fallback), obs, legal-action bitmask, next player, done, payoffs,
+                   and the final obs of every player (Env.run appends them, rlcard/envs/env.py:161-164).
+  limit.npz        same for limit-holdem (pins the stale raise_nums quirk of limitholdem/game.py:98/:101).
+  blackjack.npz    same for blackjack (+ the config-1 run_random.py trajectory: env seed 42, np.random.seed(42)).
+  doudizhu.npz     same for doudizhu (legal ids as CSR, obs padded to 901).
+  holdem_eval.npz  compare_hands winner KATs on random and category-dense 7-card deals (limitholdem/utils.py).
+  ddz_judger.npz   (hand, previous play) -> legal id sets from Judger / get_gt_cards (doudizhu/judger.py, utils.py).
+
+Usage:  python tests/golden/gen_golden.py [--only NAME ...]
+"""
+import argparse
+import hashlib
+import os
+import shutil
+import sys
+
+import numpy as np
+
+REF = '/root/reference'
+WORK = '/tmp/rlcard_amd_golden_ref'
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def setup_reference():
+    if not os.path.isdir(os.path.join(REF, 'rlcard')):
+        sys.exit('reference not found at %s (this script only runs in the build container)' % REF)
+    if os.path.isdir(WORK):
+        shutil.rmtree(WORK)
+    os.makedirs(os.path.join(WORK, 'stubs'))
+    shutil.copytree(os.path.join(REF, 'rlcard'), os.path.join(WORK, 'rlcard'))
+    with open(os.path.join(WORK, 'stubs', 'termcolor.py'), 'w') as f:
+        f.write('def colored(text, *a, **k):\n    return text\n\ndef cprint(text, *a, **k):\n    print(text)\n')
+    import typing
+    if not hasattr(typing, 'Self'):
+        typing.Self = typing.Any
+    sys.path.insert(0, os.path.join(WORK, 'stubs'))
+    sys.path.insert(0, WORK)
+    sys.dont_write_bytecode = True
+
+
+def packbits(ids, num_actions):
+    m = np.zeros(num_actions, dtype=np.uint8)
+    m[list(ids)] = 1
+    return np.packbits(m, bitorder='little')
+
+
+# --------------------------------------------------------------------------------------------------------------
+# MT19937 / seeding
+# --------------------------------------------------------------------------------------------------------------
+def gen_mt():
+    from rlcard.utils import seeding
+    seeds = [0, 1, 2, 7, 42, 43, 12941, 123456789, 2 ** 32 - 1, 2 ** 32, 2 ** 32 + 7, 2 ** 63 + 5, 2 ** 64 - 1,
+             2 ** 64 + 3]
+    keys = np.zeros((len(seeds), 2), dtype=np.uint32)
+    key_len = np.zeros(len(seeds), dtype=np.int32)
+    raw = np.zeros((len(seeds), 2000), dtype=np.uint32)
+    for i, s in enumerate(seeds):
+        k = seeding._int_list_from_bigint(seeding.hash_seed(seeding.create_seed(s)))
+        assert 1 <= len(k) <= 2
+        keys[i, :len(k)] = k
+        key_len[i] = len(k)
+        rng, _ = seeding.np_random(s)
+        raw[i] = rng.randint(0, 2 ** 32, size=2000, dtype=np.uint32)
+    # shuffles (Fisher-Yates with masked rejection) and bounded ints (randint / choice) after a fresh seed
+    shuf_n = [2, 3, 6, 52, 54, 104]
+    shuf = np.full((len(seeds), len(shuf_n), 104), -1, dtype=np.int16)
+    bounded = np.zeros((len(seeds), 64), dtype=np.int64)
+    bounded_hi = np.array([1, 2, 3, 5, 6, 7, 17, 52, 51, 100, 1000, 27471, 2, 2, 4, 9] * 4, dtype=np.int64)
+    for i, s in enumerate(seeds):
+        rng, _ = seeding.np_random(s)
+        for j, n in enumerate(shuf_n):
+            x = list(range(n))
+            rng.shuffle(x)
+            shuf[i, j, :n] = x
+        for j, hi in enumerate(bounded_hi):
+            if j % 2:
+                bounded[i, j] = rng.randint(0, hi)
+            else:
+                bounded[i, j] = rng.choice(hi)
+    # the canonical mt19937ar.c vector: init_by_array({0x123,0x234,0x345,0x456}) -> 1067595299 955945823 ...
+    r = np.random.RandomState()
+    r.seed([0x123, 0x234, 0x345, 0x456])
+    canon = r.randint(0, 2 ** 32, size=1000, dtype=np.uint32)
+    # legacy integer seeding (np.random.seed(int) -> init_genrand), used by the global agent RNG of config 1
+    r = np.random.RandomState(42)
+    genrand42 = r.randint(0, 2 ** 32, size=1000, dtype=np.uint32)
+    np.savez_compressed(os.path.join(OUT, 'mt19937.npz'),
+                        seeds=np.array([str(s) for s in seeds]), keys=keys, key_len=key_len, raw=raw,
+                        shuf_n=np.array(shuf_n, dtype=np.int32), shuf=shuf, bounded_hi=bounded_hi, bounded=bounded,
+                        canon_key=np.array([0x123, 0x234, 0x345, 0x456], dtype=np.uint32), canon=canon,
+                        genrand42=genrand42)
+    print('mt19937.npz: %d seeds' % len(seeds))
+
+
+# --------------------------------------------------------------------------------------------------------------
+# Game streams
+# --------------------------------------------------------------------------------------------------------------
+class Stream:
+    """Flat per-event record of a reference Env driven by a fixed action stream."""
+
+    def __init__(self, obs_dim, num_actions, num_players, csr_legal=False):
+        self.O, self.A, self.P, self.csr = obs_dim, num_actions, num_players, csr_legal
+        self.ev = {k: [] for k in ('env', 'game', 'kind', 'act', 'player', 'done', 'obs_len')}
+        self.obs, self.legal, self.payoff = [], [], []
+        self.legal_ids, self.legal_ptr = [], [0]
+        self.fin_game, self.fin_obs, self.fin_obs_len, self.fin_legal_n = [], [], [], []
+
+    def obs_row(self, obs):
+        o = np.zeros(self.O, dtype=np.uint8)
+        ob = np.asarray(obs)
+        assert ob.ndim == 1 and ob.size <= self.O, ob.shape
+        assert np.all((ob >= 0) & (ob <= 255)) and np.all(ob == np.round(ob)), ob
+        o[:ob.size] = ob.astype(np.int64)
+        return o, ob.size
+
+    def add(self, env_i, game_i, kind, act, state, player, done, payoffs):
+        o, n = self.obs_row(state['obs'])
+        self.ev['env'].append(env_i)
+        self.ev['game'].append(game_i)
+        self.ev['kind'].append(kind)
+        self.ev['act'].append(act)
+        self.ev['player'].append(player)
+        self.ev['done'].append(int(done))
+        self.ev['obs_len'].append(n)
+        self.obs.append(o)
+        ids = sorted(state['legal_actions'].keys())
+        if self.csr:
+            self.legal_ids.extend(ids)
+            self.legal_ptr.append(len(self.legal_ids))
+        else:
+            self.legal.append(packbits(ids, self.A))
+        p = np.zeros(self.P, dtype=np.float64)
+        if done:
+            p[:] = payoffs
+        self.payoff.append(p)
+
+    def add_final(self, game_i, states):
+        for s in states:
+            o, n = self.obs_row(s['obs'])
+            self.fin_game.append(game_i)
+            self.fin_obs.append(o)
+            self.fin_obs_len.append(n)
+            self.fin_legal_n.append(len(s['legal_actions']))
+
+    def save(self, path, seeds, **extra):
+        d = {('ev_' + k): np.array(v, dtype=np.int32) for k, v in self.ev.items()}
+        d['ev_obs'] = np.stack(self.obs)
+        d['ev_payoff'] = np.stack(self.payoff)
+        if self.csr:
+            d['ev_legal_ids'] = np.array(self.legal_ids, dtype=np.int32)
+            d['ev_legal_ptr'] = np.array(self.legal_ptr, dtype=np.int64)
+        else:
+            d['ev_legal'] = np.stack(self.legal)
+        d['fin_game'] = np.array(self.fin_game, dtype=np.int32)
+        d['fin_obs'] = np.stack(self.fin_obs)
+        d['fin_obs_len'] = np.array(self.fin_obs_len, dtype=np.int32)
+        d['fin_legal_n'] = np.array(self.fin_legal_n, dtype=np.int32)
+        d['seeds'] = np.array(seeds, dtype=np.int64)
+        d.update(extra)
+        np.savez_compressed(path, **d)
+
+
+def drive(env_id, config, seeds, games, stream, pick, extra_keys=()):
+    """For each seed: make the env once (its RNG stream continues across resets, as in the reference), then play
+    `games` games, choosing each action with pick(rng, state, env)."""
+    import random
+    import rlcard
+    game_counter = 0
+    for ei, seed in enumerate(seeds):
+        cfg = dict(config)
+        cfg['seed'] = int(seed)
+        env = rlcard.make(env_id, config=cfg)
+        rng = random.Random(1000003 * (ei + 1) + int(seed))
+        for g in range(games):
+            state, player = env.reset()
+            stream.add(ei, game_counter, 0, -1, state, player, env.is_over(), None)
+            nsteps = 0
+            while not env.is_over():
+                a = pick(rng, state, env)
+                state, player = env.step(a)
+                done = env.is_over()
+                stream.add(ei, game_counter, 1, a, state, player, done, env.get_payoffs() if done else None)
+                nsteps += 1
+                assert nsteps < 10000
+            stream.add_final(game_counter, [env.get_state(p) for p in range(env.num_players)])
+            game_counter += 1
+
+
+def pick_holdem(rng, state, env):
+    legal = sorted(state['legal_actions'].keys())
+    if rng.random() < 0.8:
+        return rng.choice(legal)
+    return rng.randrange(4)          # may be illegal: pins _decode_action (envs/leducholdem.py:81-96)
+
+
+def gen_leduc():
+    seeds = [0, 1, 2, 3, 42, 43, 12941, 2 ** 40 + 9]
+    st = Stream(36, 4, 2)
+    drive('leduc-holdem', {}, seeds, 60, st, pick_holdem)
+    st.save(os.path.join(OUT, 'leduc.npz'), seeds)
+    print('leduc.npz: %d events' % len(st.obs))
+
+
+def gen_limit():
+    seeds = [0, 1, 5, 42, 12941, 2 ** 33 + 1]
+    st = Stream(72, 4, 2)
+    drive('limit-holdem', {}, seeds, 50, st, pick_holdem)
+    st.save(os.path.join(OUT, 'limit.npz'), seeds)
+    print('limit.npz: %d events' % len(st.obs))
+
+
+def gen_blackjack():
+    seeds = [0, 1, 3, 42, 12941, 777]
+    st = Stream(2, 2, 1)
+
+    def pick(rng, state, env):
+        return rng.randrange(2)
+    drive('blackjack', {}, seeds, 60, st, pick)
+
+    # config 1: examples/run_random.py --env blackjack (env seed 42; set_seed(42) seeds the global np.random that
+    # RandomAgent draws from, rlcard/agents/random_agent.py:17-27). set_seed's torch branch is irrelevant here.
+    import rlcard
+    from rlcard.agents.random_agent import RandomAgent
+    env = rlcard.make('blackjack', config={'seed': 42})
+    np.random.seed(42)
+    agent = RandomAgent(num_actions=env.num_actions)
+    env.set_agents([agent for _ in range(env.num_players)])
+    traj, payoffs = env.run(is_training=False)
+    seq_obs, seq_act = [], []
+    for item in traj[0]:
+        if isinstance(item, dict):
+            seq_obs.append(np.asarray(item['obs'], dtype=np.int64))
+            seq_act.append(-1)
+        else:
+            seq_obs.append(np.zeros(2, dtype=np.int64))
+            seq_act.append(int(item))
+    st.save(os.path.join(OUT, 'blackjack.npz'), seeds,
+            run42_obs=np.stack(seq_obs), run42_act=np.array(seq_act, dtype=np.int32),
+            run42_payoffs=np.asarray(payoffs, dtype=np.int64))
+    print('blackjack.npz: %d events, run_random(42) trajectory length %d' % (len(st.obs), len(seq_obs)))
+
+
+def gen_doudizhu():
+    seeds = [0, 1, 42]
+    st = Stream(901, 27472, 3, csr_legal=True)
+
+    def pick(rng, state, env):
+        return rng.choice(sorted(state['legal_actions'].keys()))
+    drive('doudizhu', {}, seeds, 4, st, pick)
+    st.save(os.path.join(OUT, 'doudizhu.npz'), seeds)
+    print('doudizhu.npz: %d events' % len(st.obs))
+
+
+# --------------------------------------------------------------------------------------------------------------
+# Hold'em evaluator KATs (compare_hands, rlcard/games/limitholdem/utils.py:526-614)
+# --------------------------------------------------------------------------------------------------------------
+SUITS = 'SHDC'
+RANKS = 'A23456789TJQK'
+
+
+def card_str(c):           # card index as in limitholdem/card2index.json: suit-major S,H,D,C; rank A..K
+    return SUITS[c // 13] + RANKS[c % 13]
+
+
+def gen_holdem_eval():
+    from rlcard.games.limitholdem.utils import compare_hands
+    rng = np.random.RandomState(20251015)
+    rows, players = [], []
+    # (1) random 2-player deals from a full deck
+    for _ in range(20000):
+        d = rng.permutation(52)[:9]
+        rows.append([d[0], d[1], d[4], d[5], d[6], d[7], d[8], d[2], d[3]] + [-1] * 7)
+        players.append(2)
+    # (2) category-dense deals: restricted decks (few ranks / one suit heavy) and 3 players
+    for _ in range(20000):
+        nr = rng.randint(4, 9)
+        ranks = rng.choice(13, nr, replace=False)
+        ns = rng.randint(1, 5)
+        suits = rng.choice(4, ns, replace=False)
+        deck = np.array([s * 13 + r for s in suits for r in ranks])
+        np_ = 3 if rng.rand() < 0.3 else 2
+        need = 5 + 2 * np_
+        if len(deck) < need:
+            extra = np.setdiff1d(np.arange(52), deck)
+            deck = np.concatenate([deck, rng.choice(extra, need - len(deck), replace=False)])
+        d = rng.permutation(deck)[:need]
+        hole = [d[5 + 2 * p: 7 + 2 * p] for p in range(np_)]
+        row = list(d[:5])
+        for h in hole:
+            row += list(h)
+        rows.append(row + [-1] * (16 - len(row)))
+        players.append(np_)
+    # (3) hand-built edge cases: wheel / broadway straights, straight flush vs quads, counterfeited two pair,
+    #     three pairs, two trips, flush over straight, split boards
+    def c(s):
+        return SUITS.index(s[0]) * 13 + RANKS.index(s[1])
+    edge = [
+        (['SA', 'H2', 'D3', 'C4', 'S9'], [['H5', 'DK'], ['S6', 'C5']]),
+        (['ST', 'HJ', 'DQ', 'CK', 'S2'], [['HA', 'D3'], ['C9', 'S8']]),
+        (['S5', 'S6', 'S7', 'S8', 'H8'], [['S9', 'D2'], ['D8', 'C8']]),
+        (['S2', 'H2', 'D5', 'C5', 'S9'], [['HK', 'DK'], ['CA', 'S3']]),
+        (['S2', 'H2', 'D5', 'C5', 'S9'], [['H9', 'DQ'], ['CA', 'D9']]),
+        (['S2', 'H2', 'D2', 'C5', 'S5'], [['H5', 'DQ'], ['CA', 'DA']]),
+        (['SA', 'SK', 'SQ', 'SJ', 'H4'], [['ST', 'D2'], ['HT', 'DT']]),
+        (['S3', 'S7', 'S9', 'H4', 'D5'], [['S6', 'SJ'], ['C6', 'D8']]),
+        (['SA', 'HA', 'DA', 'CA', 'SK'], [['HQ', 'DJ'], ['C2', 'D3']]),
+        (['S2', 'H3', 'D4', 'C5', 'S6'], [['HK', 'DK'], ['CA', 'SA']]),
+        (['SK', 'HK', 'DQ', 'CQ', 'SJ'], [['HJ', 'D2'], ['CA', 'S3']]),
+        (['S9', 'H9', 'D9', 'C4', 'S4'], [['H4', 'DA'], ['C9', 'SQ']]),
+    ]
+    for board, holes in edge:
+        row = [c(x) for x in board]
+        for h in holes:
+            row += [c(x) for x in h]
+        rows.append(row + [-1] * (16 - len(row)))
+        players.append(len(holes))
+    rows = np.array(rows, dtype=np.int8)
+    players = np.array(players, dtype=np.int8)
+    winners = np.zeros((len(rows), 8), dtype=np.int8)
+    for i in range(len(rows)):
+        board = [card_str(x) for x in rows[i, :5]]
+        hands = []
+        for p in range(players[i]):
+            hands.append([card_str(x) for x in rows[i, 5 + 2 * p: 7 + 2 * p]] + board)
+        w = compare_hands(hands)
+        winners[i, :len(w)] = w
+    np.savez_compressed(os.path.join(OUT, 'holdem_eval.npz'), cards=rows, players=players, winners=winners)
+    print('holdem_eval.npz: %d deals' % len(rows))
+
+
+RANK_CHARS = '3456789TJQKA2BR'
+
+
+def gen_ddz_table():
+    """The DouDizhu action-id space (games/doudizhu/jsondata: action_space.txt, card_type.json) as numbers:
+    id -> rank counts (3..A,2,B,R), type index, weight. This is the action contract itself (27 472 ids)."""
+    from rlcard.games.doudizhu.utils import ID_2_ACTION, CARD_TYPE, TYPE_CARD
+    type_names = list(TYPE_CARD.keys())
+    n = len(ID_2_ACTION)
+    counts = np.zeros((n, 15), dtype=np.uint8)
+    ttype = np.full(n, -1, dtype=np.int16)
+    weight = np.full(n, -1, dtype=np.int16)
+    for i, a in enumerate(ID_2_ACTION):
+        if a == 'pass':
+            continue
+        for ch in a:
+            counts[i, RANK_CHARS.index(ch)] += 1
+        (t, w), = CARD_TYPE[0][a]
+        ttype[i] = type_names.index(t)
+        weight[i] = int(w)
+    digest = hashlib.sha256(' '.join(ID_2_ACTION).encode()).hexdigest()
+    np.savez_compressed(os.path.join(OUT, 'ddz_actions.npz'), counts=counts, type=ttype, weight=weight,
+                        type_names=np.array(type_names), pass_id=np.int32(ID_2_ACTION.index('pass')),
+                        action_space_sha256=np.array(digest))
+    print('ddz_actions.npz: %d ids, %d types, sha256 %s' % (n, len(type_names), digest[:16]))
+
+
+def gen_ddz_judger():
+    """Legal sets straight from the reference judger for random hands: leading = playable_cards_from_hand
+    (judger.py:124-258), following = get_gt_cards (utils.py:584-621) against a random previous play."""
+    from rlcard.games.base import Card
+    from rlcard.games.doudizhu.judger import DoudizhuJudger
+    from rlcard.games.doudizhu.utils import get_gt_cards, ACTION_2_ID, ID_2_ACTION, cards2str
+
+    class P:                                      # the two attributes get_gt_cards reads
+        def __init__(self, hand, played=None):
+            self.current_hand, self.played_cards = hand, played
+
+    def hand_of(counts):
+        cards = []
+        for r, c in enumerate(counts):
+            for k in range(c):
+                if r == 13:
+                    cards.append(Card('BJ', ''))
+                elif r == 14:
+                    cards.append(Card('RJ', ''))
+                else:
+                    cards.append(Card('SHDC'[k], RANK_CHARS[r]))
+        return cards
+
+    rng = np.random.RandomState(7)
+    deck = np.array([r for r in range(13) for _ in range(4)] + [13, 14])
+    hands, prev, ptr, ids = [], [], [0], []
+    for i in range(3000):
+        k = int(rng.choice([1, 2, 3, 4, 5, 8, 12, 17, 20, 20, 20]))
+        sel = rng.choice(54, k, replace=False)
+        cnt = np.bincount(deck[sel], minlength=15).astype(np.uint8)
+        if i % 2 == 0:
+            legal = DoudizhuJudger.playable_cards_from_hand(cards2str(hand_of(cnt)))
+            p = -1
+        else:
+            p = int(rng.randint(0, len(ID_2_ACTION) - 1))
+            legal = get_gt_cards(P(hand_of(cnt)), P(None, ID_2_ACTION[p]))
+        hands.append(cnt)
+        prev.append(p)
+        ids.extend(sorted(ACTION_2_ID[a] for a in legal))
+        ptr.append(len(ids))
+    np.savez_compressed(os.path.join(OUT, 'ddz_judger.npz'), hands=np.stack(hands), prev=np.array(prev, np.int32),
+                        legal_ptr=np.array(ptr, np.int64), legal_ids=np.array(ids, np.int32))
+    print('ddz_judger.npz: %d cases, %d legal ids' % (len(hands), len(ids)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--only', nargs='*', default=None)
+    args = ap.parse_args()
+    setup_reference()
+    gens = {'mt19937': gen_mt, 'leduc': gen_leduc, 'limit': gen_limit, 'blackjack': gen_blackjack,
+            'doudizhu': gen_doudizhu, 'holdem_eval': gen_holdem_eval, 'ddz_table': gen_ddz_table,
+            'ddz_judger': gen_ddz_judger}
+    for name, fn in gens.items():
+        if args.only is None or name in args.only:
+            fn()
+
+
+if __name__ == '__main__':
+    main()

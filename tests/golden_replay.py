@@ -1,0 +1,64 @@
+"""Replays a reference game stream (tests/golden/<game>.npz) through any engine exposing reset/step/observe on a
+single env; used for the oracle (CPU) and for the HIP engine (GPU tests)."""
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name + '.npz'), allow_pickle=False)
+
+
+def legal_bits_of(d, k, num_actions):
+    if 'ev_legal' in d.files:
+        return d['ev_legal'][k]
+    ids = d['ev_legal_ids'][d['ev_legal_ptr'][k]:d['ev_legal_ptr'][k + 1]]
+    m = np.zeros(num_actions, np.uint8)
+    m[ids] = 1
+    return np.packbits(m, bitorder='little')
+
+
+def replay(d, make_env, num_actions, check_final=True):
+    """make_env(seed_index, seed) -> object with reset() / step(a) returning dict(obs, legal, player, reward, done)
+    for one env (1-d arrays), and observe(player) -> (obs, legal). Returns the number of checked events."""
+    env_idx = d['ev_env']
+    n_checked = 0
+    cur_env, env = None, None
+    fin = {}
+    for k in range(len(env_idx)):
+        fin.setdefault(int(d['ev_game'][k]), None)
+    fin_rows = {}
+    for j, g in enumerate(d['fin_game']):
+        fin_rows.setdefault(int(g), []).append(j)
+    for k in range(len(env_idx)):
+        ei = int(env_idx[k])
+        if ei != cur_env:
+            cur_env = ei
+            env = make_env(ei, int(d['seeds'][ei]))
+        kind = int(d['ev_kind'][k])
+        out = env.reset() if kind == 0 else env.step(int(d['ev_act'][k]))
+        ctx = 'event %d (env %d game %d kind %d act %d)' % (k, ei, d['ev_game'][k], kind, d['ev_act'][k])
+        n = int(d['ev_obs_len'][k])
+        exp_obs = d['ev_obs'][k]
+        got_obs = np.asarray(out['obs']).reshape(-1)
+        assert np.array_equal(got_obs[:n], exp_obs[:n]), ctx + ' obs\n%s\n%s' % (got_obs[:n], exp_obs[:n])
+        assert not got_obs[n:].any(), ctx + ' obs padding'
+        exp_legal = legal_bits_of(d, k, num_actions)
+        got_legal = np.asarray(out['legal']).reshape(-1)
+        assert np.array_equal(got_legal, exp_legal), ctx + ' legal %s vs %s' % (
+            np.nonzero(np.unpackbits(got_legal, bitorder='little'))[0][:20],
+            np.nonzero(np.unpackbits(exp_legal, bitorder='little'))[0][:20])
+        assert int(np.asarray(out['player']).reshape(-1)[0]) == int(d['ev_player'][k]), ctx + ' player'
+        assert int(np.asarray(out['done']).reshape(-1)[0]) == int(d['ev_done'][k]), ctx + ' done'
+        if d['ev_done'][k]:
+            got_r = np.asarray(out['reward'], dtype=np.float64).reshape(-1)
+            assert np.array_equal(got_r, d['ev_payoff'][k]), ctx + ' payoff %s vs %s' % (got_r, d['ev_payoff'][k])
+            if check_final:
+                for p, j in enumerate(fin_rows[int(d['ev_game'][k])]):
+                    obs, _ = env.observe(p)
+                    m = int(d['fin_obs_len'][j])
+                    assert np.array_equal(np.asarray(obs).reshape(-1)[:m], d['fin_obs'][j][:m]), ctx + ' final obs p%d' % p
+        n_checked += 1
+    return n_checked
