@@ -1,0 +1,131 @@
+/*
+ * cardsim.h -- C ABI of the MI355X-native batched card-game engine (rlcard_amd).
+ *
+ * The reference (pmcgannon22/rlcard) has no FFI: its env path is pure Python. This ABI is the
+ * boundary a binding (ctypes here: rlcard_amd/_abi.py; cgo/JNI/N-API stubs in INTEGRATION.md) calls to replace,
+ * for a whole batch of envs at once, the reference calls listed per entry point. POD types only, 64-bit sizes,
+ * no exceptions across the boundary: every call returns CS_OK (0) or a negative CS_E_* code, and
+ * cs_last_error() returns a thread-local message for the last failure on the calling thread.
+ *
+ * Ownership: env state and the per-env MT19937 streams live in device memory owned by the handle. Every output
+ * buffer is caller-owned DEVICE memory (e.g. torch tensors' data_ptr()) with the documented shape/dtype, C-contiguous.
+ * All work is enqueued asynchronously on the caller's hipStream_t (`stream`, NULL = default stream); a handle is not
+ * thread-safe: drive it from one stream/thread. One handle per GPU.
+ */
+#ifndef RLCARD_AMD_CARDSIM_H
+#define RLCARD_AMD_CARDSIM_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    CS_OK = 0,
+    CS_E_INVALID = -1,   /* bad argument (null pointer, size, config) */
+    CS_E_DEVICE = -2,    /* HIP runtime error (no device, launch failure, out of memory) */
+    CS_E_STATE = -3,     /* call out of order (e.g. reset before seed) */
+    CS_E_UNSUPPORTED = -4
+};
+
+/* game ids; names as registered by rlcard/envs/__init__.py:6-54 */
+enum { CS_GAME_BLACKJACK = 0, CS_GAME_LEDUC = 1, CS_GAME_LIMIT = 2, CS_GAME_DOUDIZHU = 3 };
+
+typedef struct cs_handle cs_handle;
+
+/* Game configuration: the 'game_*' keys Env.__init__ forwards to Game.configure (rlcard/envs/env.py:33-39). */
+typedef struct {
+    int32_t num_players; /* blackjack 'game_num_players' (default 1); leduc/limit 2; doudizhu 3 (0 = default) */
+    int32_t num_decks;   /* blackjack 'game_num_decks' (default 1, 0 = infinite); ignored elsewhere (-1 = default) */
+    int32_t reserved[6];
+} cs_config;
+
+/* Static shape of a game (rlcard Env.num_players / num_actions / state_shape). */
+typedef struct {
+    int32_t obs_dim;      /* bytes per obs row: leduc 36, limit 72, blackjack 2, doudizhu 901 (landlord rows use 790) */
+    int32_t num_actions;  /* leduc/limit 4, blackjack 2, doudizhu 27472 */
+    int32_t num_players;
+    int32_t legal_bytes;  /* ceil(num_actions / 8): legal-action bitmask bytes per row */
+    int32_t action_bytes; /* dtype width of rollout action rows: 1 (uint8) or 2 (int16, doudizhu) */
+    int32_t state_words;  /* packed u32 words of game state per env */
+    int32_t reserved[2];
+} cs_game_info;
+
+/* Outputs of reset/step/observe, all device pointers, one row per env:
+ *   obs    uint8  [n][obs_dim]     the current player's observation (values 0/1; blackjack: the two scores)
+ *   legal  uint8  [n][legal_bytes] legal-action bitmask, bit a of byte a/8 (LSB first) = action id a
+ *   player uint8  [n]              current player id (Env.get_player_id)
+ *   reward float  [n][num_players] payoffs of the transition (non-zero only where done; Env.get_payoffs)
+ *   done   uint8  [n]              1 if the game is over after this call (Env.is_over)
+ * Any pointer may be NULL to skip that output. */
+typedef struct {
+    void* obs;
+    void* legal;
+    void* player;
+    void* reward;
+    void* done;
+} cs_step_out;
+
+/* Rollout trajectory, all device pointers, rows [T][n]:
+ *   obs [T][n][obs_dim] u8, legal [T][n][legal_bytes] u8, player [T][n] u8 (the acting player's pre-step view),
+ *   action [T][n] (uint8 or int16 per cs_game_info.action_bytes), reward [T][n][num_players] f32, done [T][n] u8. */
+typedef struct {
+    void* obs;
+    void* legal;
+    void* player;
+    void* action;
+    void* reward;
+    void* done;
+} cs_traj_out;
+
+/* Shape of a game under a config. Replaces reading Env.num_players / num_actions / state_shape. */
+int cs_game_info_get(int32_t game, const cs_config* cfg, cs_game_info* info);
+
+/* Create n envs of `game` on HIP device `device`. Replaces rlcard.make(env_id, config) (envs/registration.py:77-89)
+ * for n independent envs; allocates state (state_words*4 B/env) + MT19937 streams (4992 B/env) in HBM. */
+int cs_create(cs_handle** out, int32_t game, int64_t num_envs, int32_t device, const cs_config* cfg);
+void cs_destroy(cs_handle* h);
+
+/* Seed envs [first_env, first_env + n) from init_by_array keys computed on the host from each env's seed
+ * (rlcard/utils/seeding.py:33-113): keys [n][2] u32 (HOST memory), key_len [n] (1 or 2). Replaces Env.seed(seed)
+ * (envs/env.py:228-231). Marks those envs as finished (the next reset/step starts a game). */
+int cs_seed(cs_handle* h, const uint32_t* keys, const int32_t* key_len, int64_t first_env, int64_t n, void* stream);
+
+/* Start a new game in every env. Replaces Env.reset() (envs/env.py:52-63) -> Game.init_game + _extract_state. */
+int cs_reset(cs_handle* h, const cs_step_out* out, void* stream);
+
+/* One Env.step (envs/env.py:65-86) per env with actions [n] int32 (DEVICE memory). Illegal ids follow the
+ * reference's _decode_action (envs/leducholdem.py:81-96, limitholdem.py:81-96). Envs whose game was already over
+ * start a new game instead (lazy auto-reset: action ignored, done = 0, reward = 0), so an RL loop never calls
+ * reset() per env. */
+int cs_step(cs_handle* h, const int32_t* actions, const cs_step_out* out, void* stream);
+
+/* Observation of `player` in every env without changing state. Replaces Env.get_state(player_id)
+ * (envs/env.py:188-197), e.g. the final states Env.run appends for every player (env.py:161-164). */
+int cs_observe(cs_handle* h, int32_t player, const cs_step_out* out, void* stream);
+
+/* T fused lockstep steps with an in-kernel uniform-random policy over the legal actions (the random-agent
+ * benchmark policy of examples/run_random.py, agents/random_agent.py:17-47, with the global np.random replaced by
+ * Philox4x32-10 keyed by (policy_seed) on counter (env_base + env, t0 + t)). A finished game restarts immediately.
+ * Replaces T iterations of the Env.run loop (envs/env.py:120-169) for every env. */
+int cs_rollout(cs_handle* h, int32_t T, uint64_t policy_seed, uint64_t t0, uint64_t env_base, const cs_traj_out* out,
+               void* stream);
+
+/* Copy the packed state words of env `env` (state_words u32, HOST buffer) -- the raw fields behind
+ * Env.get_state()['raw_obs'] / get_perfect_information for single-env compatibility and debugging. Synchronous. */
+int cs_get_env_state(cs_handle* h, int64_t env, uint32_t* host_words, int32_t nwords);
+
+/* Stream position (u32 draws consumed) bookkeeping word of env `env` (HOST out). Synchronous; for parity tests. */
+int cs_get_rng_ctl(cs_handle* h, int64_t env, uint32_t* host_ctl);
+
+/* Testing hook: when enabled, the wave-cooperative MT refill is skipped, so every block crossing takes the in-lane
+ * serial twist; results must be identical. */
+int cs_debug_set_serial_refill(cs_handle* h, int32_t enable);
+
+const char* cs_last_error(void);
+const char* cs_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

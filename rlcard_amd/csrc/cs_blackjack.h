@@ -1,0 +1,186 @@
+// cs_blackjack.h -- Blackjack (1..4 players, 1 deck or infinite deck) as a lane-per-env lockstep state machine.
+//
+// Behaviour (reference file:line):
+//   rlcard/games/blackjack/dealer.py:4-37   52-card deck shuffled once per game (np.array + np_random.shuffle); deal_card:
+//                                           idx = np_random.choice(len(deck)), card = deck[idx], deck.pop(idx) unless
+//                                           num_decks == 0 (infinite deck: the card stays)
+//   rlcard/games/blackjack/game.py:22-54    init_game: two rounds of (player 0..P-1, dealer); judge_round all
+//   rlcard/games/blackjack/game.py:56-123   step: any action but 'stand' hits; a bust or a stand by the last player
+//                                           makes the dealer draw while score < 17, then judge_game for every player
+//   rlcard/games/blackjack/game.py:160-205  state: own hand; dealer hand[1:] until the game is over; is_over
+//   rlcard/games/blackjack/judger.py:2-73   scores with soft aces; winner codes 2 / 1 / -1
+//   rlcard/envs/blackjack.py:38-103         obs = [score(own), score(dealer visible)], legal {hit, stand}, payoff 1/0/-1
+// The deck (52 bytes) and the hands stay in HBM between calls; inside a kernel they live in a per-lane LDS scratch
+// (lane-interleaved words, so uniform word indices are bank-conflict free) because dealing indexes them dynamically.
+// "deck.pop(idx)" is an order-statistic removal: a 52-bit removed mask over the shuffled positions; the idx-th
+// remaining card is the idx-th clear bit.
+// Packed state, 32 u32 words per env (word-major [32][N]):
+//   0..12  shuffled deck, card id (S,H,D,C x A..K) per byte
+//   13     removed mask bits 0..31;  14: removed bits 32..51 | deck_len << 20 | game_pointer << 26 | over << 29
+//   15..29 hands: hand h (players 0..P-1, dealer = P) bytes 12h .. 12h+11
+//   30     hand sizes 4 bits each (5 hands) | winner codes 2 bits per player << 20 (0 none, 1 tie, 2 win, 3 loss)
+#pragma once
+#include "cs_device.h"
+
+namespace cs {
+
+template <int NP>
+struct Blackjack {
+    static constexpr int OBS = 2, A = 2, P = NP, LB = 1, WORDS = 32, ACTION_BYTES = 1;
+    static constexpr int NB = 1;               // raw obs dwords
+    static constexpr bool RAW_OBS = true;      // observe() returns byte values, not a 0/1 bitmap
+    static constexpr int SCRATCH_WORDS = WORDS;
+    static constexpr int HAND_CAP = 12;
+
+    uint32_t* s;   // lane scratch: word i at s[i * WAVE]
+    int infinite;
+
+    __device__ __forceinline__ uint32_t& W(int i) const { return s[i * WAVE]; }
+    __device__ __forceinline__ int byte_at(int word0, int k) const { return (W(word0 + (k >> 2)) >> (8 * (k & 3))) & 255; }
+    __device__ __forceinline__ void set_byte(int word0, int k, int v) const
+    {
+        uint32_t& w = W(word0 + (k >> 2));
+        const int sh = 8 * (k & 3);
+        w = (w & ~(255u << sh)) | ((uint32_t)v << sh);
+    }
+
+    __device__ __forceinline__ void bind(uint32_t* lane_scratch, const GameParams& prm)
+    {
+        s = lane_scratch;
+        infinite = prm.num_decks == 0;
+    }
+    __device__ __forceinline__ void load(const uint32_t* st, int64_t n, int64_t env)
+    {
+#pragma unroll
+        for (int i = 0; i < WORDS; i++) W(i) = st[(int64_t)i * n + env];
+    }
+    __device__ __forceinline__ void store(uint32_t* st, int64_t n, int64_t env) const
+    {
+#pragma unroll
+        for (int i = 0; i < WORDS; i++) st[(int64_t)i * n + env] = W(i);
+    }
+    __device__ __forceinline__ void blank()
+    {
+#pragma unroll
+        for (int i = 0; i < WORDS; i++) W(i) = 0;
+        W(14) = 1u << 29;
+    }
+
+    __device__ __forceinline__ int nhand(int h) const { return (W(30) >> (4 * h)) & 15; }
+    __device__ __forceinline__ int winner(int p) const { return (W(30) >> (20 + 2 * p)) & 3; }
+    __device__ __forceinline__ int current() const { return (W(14) >> 26) & 7; }
+    __device__ __forceinline__ bool is_over() const { return (W(14) >> 29) & 1; }
+    __device__ __forceinline__ uint32_t legal() const { return 3u; }
+
+    __device__ static __forceinline__ int card_value(int c)
+    {
+        const int r = c % 13;
+        return r == 0 ? 11 : (r >= 9 ? 10 : r + 1);
+    }
+    // judge_score over cards [from, n) of hand h
+    __device__ __forceinline__ int score(int h, int from) const
+    {
+        int sc = 0, aces = 0;
+        const int n = nhand(h);
+        for (int k = from; k < n; k++) {
+            const int c = byte_at(15, HAND_CAP * h + k);
+            sc += card_value(c);
+            aces += (c % 13) == 0;
+        }
+        while (sc > 21 && aces > 0) { aces--; sc -= 10; }
+        return sc;
+    }
+
+    __device__ __forceinline__ void deal(MtLane& rng, int h)
+    {
+        const int len = (W(14) >> 20) & 63;
+        const int idx = (int)rng.interval((uint32_t)(len - 1));
+        uint64_t avail = ~((uint64_t)W(13) | (uint64_t)(W(14) & 0xFFFFFu) << 32) & ((1ull << 52) - 1);
+        for (int k = 0; k < idx; k++) avail &= avail - 1;
+        const int pos = __builtin_ctzll(avail);
+        const int c = byte_at(0, pos);
+        if (!infinite) {
+            if (pos < 32) W(13) |= 1u << pos;
+            else W(14) |= 1u << (pos - 32);
+            W(14) = (W(14) & ~(63u << 20)) | ((uint32_t)(len - 1) << 20);
+        }
+        const int n = nhand(h);
+        if (n < HAND_CAP) {      // 12 cards always bust a 1-deck hand before this bound
+            set_byte(15, HAND_CAP * h + n, c);
+            W(30) += 1u << (4 * h);
+        }
+    }
+
+    __device__ __forceinline__ void observe(int player, uint32_t (&raw)[NB]) const
+    {
+        const int mine = score(player, 0);
+        const int dealer = is_over() ? score(NP, 0) : score(NP, 1);
+        raw[0] = (uint32_t)mine | (uint32_t)dealer << 8;
+    }
+
+    __device__ __forceinline__ void reset(MtLane& rng)
+    {
+        // 52-card Fisher-Yates in the deck words (bytes), then the initial deal
+#pragma unroll
+        for (int w = 0; w < 13; w++) W(w) = (uint32_t)(4 * w) | (uint32_t)(4 * w + 1) << 8 | (uint32_t)(4 * w + 2) << 16 |
+                                            (uint32_t)(4 * w + 3) << 24;
+        for (int i = 51; i >= 1; i--) {
+            const int j = (int)rng.interval((uint32_t)i);
+            const int ci = byte_at(0, i), cj = byte_at(0, j);
+            set_byte(0, i, cj);
+            set_byte(0, j, ci);
+        }
+        W(13) = 0;
+        W(14) = 52u << 20;
+#pragma unroll
+        for (int w = 15; w <= 30; w++) W(w) = 0;
+        for (int r = 0; r < 2; r++) {
+            for (int j = 0; j < NP; j++) deal(rng, j);
+            deal(rng, NP);
+        }
+    }
+
+    __device__ __forceinline__ void finish(MtLane& rng)
+    {
+        while (score(NP, 0) < 17) deal(rng, NP);
+        const int d = score(NP, 0);
+        uint32_t win = 0;
+        for (int p = 0; p < NP; p++) {
+            const int sp = score(p, 0);
+            int code;
+            if (sp > 21) code = 3;
+            else if (d > 21) code = 2;
+            else if (sp > d) code = 2;
+            else if (sp < d) code = 3;
+            else code = 1;
+            win |= (uint32_t)code << (20 + 2 * p);
+        }
+        W(30) = (W(30) & 0xFFFFFu) | win;
+        W(14) = (W(14) & ~(7u << 26)) | 1u << 29;   // game_pointer = 0, over
+    }
+
+    __device__ __forceinline__ void step(int a, MtLane& rng)
+    {
+        const int gp = current();
+        bool advance = true;
+        if (a != 1) {
+            deal(rng, gp);
+            advance = score(gp, 0) > 21;
+        }
+        if (advance) {
+            if (gp >= NP - 1) finish(rng);
+            else W(14) = (W(14) & ~(7u << 26)) | (uint32_t)(gp + 1) << 26;
+        }
+    }
+
+    __device__ __forceinline__ void payoffs(float (&r)[P]) const
+    {
+#pragma unroll
+        for (int p = 0; p < NP; p++) {
+            const int w = winner(p);
+            r[p] = w == 2 ? 1.f : (w == 1 ? 0.f : -1.f);
+        }
+    }
+};
+
+}  // namespace cs

@@ -1,0 +1,32 @@
+// cs_engine.h -- internal interface between the C ABI (cs_abi.cpp) and the kernels (cs_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/cardsim.h"
+
+namespace cs {
+
+constexpr int MT_WORDS_HOST = 2 * 624;  // u32 per env: two MT19937 blocks
+
+struct Buffers {
+    int32_t game;
+    int64_t n;
+    uint32_t* mt;     // [n][1248]
+    uint32_t* ctl;    // [n]
+    uint32_t* state;  // [state_words][n]
+    const void* table;  // game-specific read-only table (doudizhu action table), or null
+    int32_t num_players, num_decks;
+    int32_t serial_refill;  // testing hook
+};
+
+int game_info(int32_t game, const cs_config* cfg, cs_game_info* info);
+
+hipError_t launch_seed(const Buffers& b, const uint32_t* keys_dev, const int32_t* klen_dev, int64_t first,
+                       int64_t count, hipStream_t s);
+hipError_t launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s);
+hipError_t launch_step(const Buffers& b, const int32_t* actions, const cs_step_out& o, hipStream_t s);
+hipError_t launch_observe(const Buffers& b, int32_t player, const cs_step_out& o, hipStream_t s);
+hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
+                          const cs_traj_out& o, hipStream_t s);
+
+}  // namespace cs

@@ -1,0 +1,457 @@
+// cs_kernels.hip -- lockstep env kernels for gfx950 (one lane = one env, one wave = 64 consecutive envs).
+//
+// Every kernel is the same skeleton over a Game type (cs_leduc.h, ...):
+//   load packed state (word-major SoA, coalesced) -> per step: observe / legal / pick / emit rows / step / payoffs /
+//   auto-reset -> wave-cooperative MT19937 refill at the step boundary -> store state.
+// Integer/branchy work: no MFMA. The bound is HBM (obs/legal/reward rows out, packed state + RNG words in/out).
+#include "cs_device.h"
+#include "cs_engine.h"
+#include "cs_leduc.h"
+#include "cs_limit.h"
+#include "cs_blackjack.h"
+
+namespace cs {
+
+constexpr int BLOCK = 256;
+constexpr int WAVES_PER_BLOCK = BLOCK / WAVE;
+
+__device__ inline void mt_init_by_array(uint32_t* mt, const uint32_t* key, int klen)
+{
+    uint32_t prev = 19650218u;
+    mt[0] = prev;
+    for (int i = 1; i < MT_N; i++) {
+        prev = 1812433253u * (prev ^ (prev >> 30)) + (uint32_t)i;
+        mt[i] = prev;
+    }
+    int i = 1, j = 0;
+    prev = mt[0];
+    for (int k = MT_N; k; k--) {
+        const uint32_t v = (mt[i] ^ ((prev ^ (prev >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
+        mt[i] = v;
+        prev = v;
+        i++;
+        j++;
+        if (i >= MT_N) { mt[0] = mt[MT_N - 1]; prev = mt[0]; i = 1; }
+        if (j >= klen) j = 0;
+    }
+    for (int k = MT_N - 1; k; k--) {
+        const uint32_t v = (mt[i] ^ ((prev ^ (prev >> 30)) * 1566083941u)) - (uint32_t)i;
+        mt[i] = v;
+        prev = v;
+        i++;
+        if (i >= MT_N) { mt[0] = mt[MT_N - 1]; prev = mt[0]; i = 1; }
+    }
+    mt[0] = 0x80000000u;
+}
+
+struct LaneCtx {
+    int lane, wid;
+    int64_t env, wave_first;
+    int nvalid;
+    bool valid;
+};
+
+__device__ __forceinline__ LaneCtx lane_ctx(int64_t n)
+{
+    LaneCtx c;
+    c.lane = threadIdx.x & (WAVE - 1);
+    c.wid = threadIdx.x / WAVE;
+    c.env = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    c.wave_first = c.env - c.lane;
+    const int64_t left = n - c.wave_first;
+    c.nvalid = left >= WAVE ? WAVE : (int)left;
+    c.valid = c.env < n;
+    return c;
+}
+
+__device__ __forceinline__ MtLane mt_lane(uint32_t* mt, const uint32_t* ctl, const LaneCtx& c)
+{
+    MtLane m;
+    if (c.valid) {
+        const uint32_t w = ctl[c.env];
+        m.base = mt + c.env * MT_WORDS;
+        m.pos = w & 0x7ffu;
+        m.stale = (w >> 16) & 1u;
+    } else {
+        m.base = mt;
+        m.pos = 0;
+        m.stale = 0;
+    }
+    return m;
+}
+
+__device__ __forceinline__ void refill(MtLane& m, int lane, int serial_only)
+{
+    if (!serial_only) mt_refill_wave(m, lane);
+}
+
+// obs rows: staged + coalesced when the row is a dword multiple, per-lane bytes otherwise
+template <class G>
+__device__ __forceinline__ void emit_obs(uint32_t* lds, const uint32_t (&bits)[G::NB], uint8_t* obs, int64_t row0,
+                                         const LaneCtx& c)
+{
+    if constexpr (G::RAW_OBS) {
+        if (c.valid) {
+            uint8_t* o = obs + (row0 + c.lane) * G::OBS;
+#pragma unroll
+            for (int k = 0; k < G::OBS; k++) o[k] = (uint8_t)(bits[k >> 2] >> (8 * (k & 3)));
+        }
+    } else if constexpr (G::OBS % 4 == 0) {
+        RowWriter<G::OBS>::write(lds, bits, obs + row0 * G::OBS, c.lane, c.nvalid);
+    } else {
+        if (c.valid) {
+            uint8_t* o = obs + (row0 + c.lane) * G::OBS;
+#pragma unroll
+            for (int k = 0; k < G::OBS; k++) o[k] = (uint8_t)((bits[k >> 5] >> (k & 31)) & 1u);
+        }
+    }
+}
+
+template <class G>
+__device__ __forceinline__ void emit_legal(uint8_t* legal, int64_t row, uint64_t lg)
+{
+#pragma unroll
+    for (int k = 0; k < G::LB; k++) legal[row * G::LB + k] = (uint8_t)(lg >> (8 * k));
+}
+
+template <class G>
+__device__ __forceinline__ void emit_reward(float* reward, int64_t row, const float (&r)[G::P])
+{
+    if constexpr (G::P == 2) {
+        *(float2*)(reward + row * 2) = make_float2(r[0], r[1]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < G::P; k++) reward[row * G::P + k] = r[k];
+    }
+}
+
+template <int ROW, bool STAGED>
+struct ObsWords {
+    static constexpr int value = 1;
+};
+template <int ROW>
+struct ObsWords<ROW, true> {
+    static constexpr int value = RowWriter<ROW>::LDS_WORDS;
+};
+template <class G>
+struct ObsLds {
+    static constexpr int WORDS = ObsWords<G::OBS, !G::RAW_OBS && G::OBS % 4 == 0>::value;
+};
+template <class G>
+struct Scratch {
+    static constexpr int WORDS = (G::SCRATCH_WORDS > 0 ? G::SCRATCH_WORDS : 1) * WAVE;
+};
+#define CS_SMEM(G)                                                  \
+    __shared__ uint32_t lds[WAVES_PER_BLOCK][ObsLds<G>::WORDS];     \
+    __shared__ uint32_t scr[WAVES_PER_BLOCK][Scratch<G>::WORDS]
+
+// ------------------------------------------------------------------------------------------------------------------
+template <class G>
+__global__ __launch_bounds__(BLOCK) void k_seed(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
+                                                 const uint32_t* keys, const int32_t* klen, int64_t first,
+                                                 int64_t count, int serial_only, GameParams prm)
+{
+    __shared__ uint32_t scr[WAVES_PER_BLOCK][Scratch<G>::WORDS];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const bool valid = i < count;
+    const int64_t env = first + i;
+    MtLane m;
+    m.base = mt;
+    m.pos = 0;
+    m.stale = 0;
+    if (valid) {
+        uint32_t* base = mt + env * MT_WORDS;
+        const int kl = klen[i] == 2 ? 2 : 1;                    // validated on the host; never trust it here
+        mt_init_by_array(base + MT_N, keys + 2 * i, kl);        // S0 in block 1 (scratch)
+        mt_twist_serial(base + MT_N, base);                     // block 0 = twist(S0): numpy's first draws
+        m.base = base;
+        m.stale = 1;                                            // block 1 = twist(block 0), refilled below
+        G g;
+        g.bind(&scr[threadIdx.x / WAVE][lane], prm);
+        g.blank();
+        g.store(st, n, env);
+    }
+    if (serial_only) {
+        if (valid) mt_twist_serial(m.base, m.base + MT_N);
+        m.stale = 0;
+    } else {
+        mt_refill_wave(m, lane);
+    }
+    if (valid) ctl[env] = 0u;
+}
+
+template <class G>
+__global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
+                                                  cs_step_out out, int serial_only, GameParams prm)
+{
+    CS_SMEM(G);
+    const LaneCtx c = lane_ctx(n);
+    MtLane m = mt_lane(mt, ctl, c);
+    G g;
+    g.bind(&scr[c.wid][c.lane], prm);
+    g.blank();
+    if (c.valid) {
+        g.load(st, n, c.env);   // the Game object outlives init_game (limit-holdem's raise history, :98/:101)
+        g.reset(m);
+    }
+    refill(m, c.lane, serial_only);
+    uint32_t bits[G::NB];
+    const int p = g.current();
+    g.observe(p, bits);
+    if (out.obs) emit_obs<G>(lds[c.wid], bits, (uint8_t*)out.obs, c.wave_first, c);
+    if (c.valid) {
+        if (out.legal) emit_legal<G>((uint8_t*)out.legal, c.env, g.legal());
+        if (out.player) ((uint8_t*)out.player)[c.env] = (uint8_t)p;
+        if (out.reward) {
+            float r[G::P];
+#pragma unroll
+            for (int k = 0; k < G::P; k++) r[k] = 0.f;
+            emit_reward<G>((float*)out.reward, c.env, r);
+        }
+        if (out.done) ((uint8_t*)out.done)[c.env] = (uint8_t)g.is_over();
+        g.store(st, n, c.env);
+        ctl[c.env] = m.pos | (m.stale << 16);
+    }
+}
+
+template <class G>
+__global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
+                                                 const int32_t* actions, cs_step_out out, int serial_only,
+                                                 GameParams prm)
+{
+    CS_SMEM(G);
+    const LaneCtx c = lane_ctx(n);
+    MtLane m = mt_lane(mt, ctl, c);
+    G g;
+    g.bind(&scr[c.wid][c.lane], prm);
+    g.blank();
+    float r[G::P];
+#pragma unroll
+    for (int k = 0; k < G::P; k++) r[k] = 0.f;
+    bool done = false;
+    if (c.valid) {
+        g.load(st, n, c.env);
+        if (g.is_over()) {
+            g.reset(m);
+        } else {
+            g.step(actions[c.env], m);
+            done = g.is_over();
+            if (done) g.payoffs(r);
+        }
+    }
+    refill(m, c.lane, serial_only);
+    uint32_t bits[G::NB];
+    const int p = g.current();
+    g.observe(p, bits);
+    if (out.obs) emit_obs<G>(lds[c.wid], bits, (uint8_t*)out.obs, c.wave_first, c);
+    if (c.valid) {
+        if (out.legal) emit_legal<G>((uint8_t*)out.legal, c.env, g.legal());
+        if (out.player) ((uint8_t*)out.player)[c.env] = (uint8_t)p;
+        if (out.reward) emit_reward<G>((float*)out.reward, c.env, r);
+        if (out.done) ((uint8_t*)out.done)[c.env] = (uint8_t)done;
+        g.store(st, n, c.env);
+        ctl[c.env] = m.pos | (m.stale << 16);
+    }
+}
+
+template <class G>
+__global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n, int player, cs_step_out out,
+                                                    GameParams prm)
+{
+    CS_SMEM(G);
+    const LaneCtx c = lane_ctx(n);
+    G g;
+    g.bind(&scr[c.wid][c.lane], prm);
+    g.blank();
+    if (c.valid) g.load(st, n, c.env);
+    uint32_t bits[G::NB];
+    g.observe(player, bits);
+    if (out.obs) emit_obs<G>(lds[c.wid], bits, (uint8_t*)out.obs, c.wave_first, c);
+    if (c.valid) {
+        if (out.legal) emit_legal<G>((uint8_t*)out.legal, c.env, g.legal());
+        if (out.player) ((uint8_t*)out.player)[c.env] = (uint8_t)g.current();
+        if (out.done) ((uint8_t*)out.done)[c.env] = (uint8_t)g.is_over();
+    }
+}
+
+template <class G>
+__global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n, int T,
+                                                    uint64_t seed, uint64_t t0, uint64_t env_base, cs_traj_out out,
+                                                    int serial_only, GameParams prm)
+{
+    CS_SMEM(G);
+    const LaneCtx c = lane_ctx(n);
+    MtLane m = mt_lane(mt, ctl, c);
+    G g;
+    g.bind(&scr[c.wid][c.lane], prm);
+    g.blank();
+    if (c.valid) {
+        g.load(st, n, c.env);
+        if (g.is_over()) g.reset(m);
+    }
+    refill(m, c.lane, serial_only);
+    uint8_t* obs = (uint8_t*)out.obs;
+    uint8_t* legal = (uint8_t*)out.legal;
+    uint8_t* player = (uint8_t*)out.player;
+    float* reward = (float*)out.reward;
+    uint8_t* done_o = (uint8_t*)out.done;
+    const uint64_t genv = env_base + (uint64_t)c.env;
+    for (int t = 0; t < T; t++) {
+        const int64_t rowbase = (int64_t)t * n;
+        const int p = g.current();
+        const uint64_t lg = g.legal();
+        uint32_t bits[G::NB];
+        g.observe(p, bits);
+        const int a = pick_legal(lg, philox_u32(seed, genv, t0 + (uint64_t)t));
+        emit_obs<G>(lds[c.wid], bits, obs, rowbase + c.wave_first, c);
+        float r[G::P];
+#pragma unroll
+        for (int k = 0; k < G::P; k++) r[k] = 0.f;
+        bool done = false;
+        if (c.valid) {
+            const int64_t row = rowbase + c.env;
+            emit_legal<G>(legal, row, lg);
+            player[row] = (uint8_t)p;
+            if constexpr (G::ACTION_BYTES == 1) ((uint8_t*)out.action)[row] = (uint8_t)a;
+            else ((int16_t*)out.action)[row] = (int16_t)a;
+            g.step(a, m);
+            done = g.is_over();
+            if (done) g.payoffs(r);
+            emit_reward<G>(reward, row, r);
+            done_o[row] = (uint8_t)done;
+            if (done) g.reset(m);
+        }
+        refill(m, c.lane, serial_only);
+    }
+    if (c.valid) {
+        g.store(st, n, c.env);
+        ctl[c.env] = m.pos | (m.stale << 16);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+static inline GameParams params_of(const Buffers& b) { return GameParams{b.num_players, b.num_decks}; }
+static inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + BLOCK - 1) / BLOCK)); }
+
+template <class G>
+static hipError_t seed_g(const Buffers& b, const uint32_t* keys, const int32_t* klen, int64_t first, int64_t count,
+                         hipStream_t s)
+{
+    hipLaunchKernelGGL(k_seed<G>, grid_for(count), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, keys, klen, first,
+                       count, b.serial_refill, params_of(b));
+    return hipGetLastError();
+}
+template <class G>
+static hipError_t reset_g(const Buffers& b, const cs_step_out& o, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_reset<G>, grid_for(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, o, b.serial_refill, params_of(b));
+    return hipGetLastError();
+}
+template <class G>
+static hipError_t step_g(const Buffers& b, const int32_t* a, const cs_step_out& o, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_step<G>, grid_for(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, a, o, b.serial_refill,
+                       params_of(b));
+    return hipGetLastError();
+}
+template <class G>
+static hipError_t observe_g(const Buffers& b, int32_t p, const cs_step_out& o, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_observe<G>, grid_for(b.n), dim3(BLOCK), 0, s, b.state, b.n, p, o, params_of(b));
+    return hipGetLastError();
+}
+template <class G>
+static hipError_t rollout_g(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
+                            const cs_traj_out& o, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_rollout<G>, grid_for(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0,
+                       env_base, o, b.serial_refill, params_of(b));
+    return hipGetLastError();
+}
+
+template <class G>
+static void fill_info(cs_game_info* info)
+{
+    info->obs_dim = G::OBS;
+    info->num_actions = G::A;
+    info->num_players = G::P;
+    info->legal_bytes = G::LB;
+    info->action_bytes = G::ACTION_BYTES;
+    info->state_words = G::WORDS;
+}
+
+int game_info(int32_t game, const cs_config* cfg, cs_game_info* info)
+{
+    switch (game) {
+    case CS_GAME_LEDUC:
+        if (cfg && cfg->num_players != 0 && cfg->num_players != 2) return CS_E_UNSUPPORTED;
+        fill_info<Leduc>(info);
+        return CS_OK;
+    case CS_GAME_LIMIT:
+        if (cfg && cfg->num_players != 0 && cfg->num_players != 2) return CS_E_UNSUPPORTED;
+        fill_info<Limit>(info);
+        return CS_OK;
+    case CS_GAME_BLACKJACK: {
+        const int np = (cfg && cfg->num_players > 0) ? cfg->num_players : 1;
+        const int nd = (cfg && cfg->num_decks >= 0) ? cfg->num_decks : 1;
+        if (np > 4 || nd > 1) return CS_E_UNSUPPORTED;
+        if (np == 1) fill_info<Blackjack<1>>(info);
+        else if (np == 2) fill_info<Blackjack<2>>(info);
+        else if (np == 3) fill_info<Blackjack<3>>(info);
+        else fill_info<Blackjack<4>>(info);
+        return CS_OK;
+    }
+    default:
+        return CS_E_UNSUPPORTED;
+    }
+}
+
+#define CS_DISPATCH(game, CALL)                                  \
+    switch (game) {                                              \
+    case CS_GAME_LEDUC: return CALL(Leduc);                      \
+    case CS_GAME_LIMIT: return CALL(Limit);                      \
+    case CS_GAME_BLACKJACK:                                      \
+        switch (b.num_players) {                                 \
+        case 1: return CALL(Blackjack<1>);                       \
+        case 2: return CALL(Blackjack<2>);                       \
+        case 3: return CALL(Blackjack<3>);                       \
+        default: return CALL(Blackjack<4>);                      \
+        }                                                        \
+    default: return hipErrorInvalidValue;                        \
+    }
+
+hipError_t launch_seed(const Buffers& b, const uint32_t* keys, const int32_t* klen, int64_t first, int64_t count,
+                       hipStream_t s)
+{
+#define C_(G) seed_g<G>(b, keys, klen, first, count, s)
+    CS_DISPATCH(b.game, C_)
+#undef C_
+}
+hipError_t launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s)
+{
+#define C_(G) reset_g<G>(b, o, s)
+    CS_DISPATCH(b.game, C_)
+#undef C_
+}
+hipError_t launch_step(const Buffers& b, const int32_t* a, const cs_step_out& o, hipStream_t s)
+{
+#define C_(G) step_g<G>(b, a, o, s)
+    CS_DISPATCH(b.game, C_)
+#undef C_
+}
+hipError_t launch_observe(const Buffers& b, int32_t p, const cs_step_out& o, hipStream_t s)
+{
+#define C_(G) observe_g<G>(b, p, o, s)
+    CS_DISPATCH(b.game, C_)
+#undef C_
+}
+hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
+                          const cs_traj_out& o, hipStream_t s)
+{
+#define C_(G) rollout_g<G>(b, T, seed, t0, env_base, o, s)
+    CS_DISPATCH(b.game, C_)
+#undef C_
+}
+
+}  // namespace cs

@@ -1,0 +1,239 @@
+// cs_limit.h -- Limit Texas Hold'em (2 players) as a lane-per-env lockstep state machine.
+//
+// Behaviour (reference file:line):
+//   rlcard/utils/utils.py:34-43                standard deck: suits S,H,D,C x ranks A..K  (card id = card2index)
+//   rlcard/games/limitholdem/dealer.py:4-21    shuffle at construction, deal_card = deck.pop()
+//   rlcard/games/limitholdem/game.py:46-103    init_game: hole i -> player i%2 from deck[51-i]; SB = randint(0,2);
+//                                              first actor (BB+1)%2; the reset obs carries the PREVIOUS game's
+//                                              raise counts (get_state at :98 runs before history_raise_nums is
+//                                              re-bound at :101) -- kept as prev_raise_nums + use_prev
+//   rlcard/games/limitholdem/game.py:105-158   step: history_raise_nums[round] = have_raised; flop deck[47..45],
+//                                              turn deck[44], river deck[43]; raise amount 2 -> 4 after round 1
+//   rlcard/games/limitholdem/round.py:53-127   betting FSM, allowed_raise_num = 4
+//   rlcard/games/limitholdem/game.py:216-243   is_over: one alive or round_counter >= 4; payoffs / big_blind
+//   rlcard/games/limitholdem/judger.py:11-108  pot split (2 players: the winner nets the loser's bet, ties return
+//                                              the bets, np_random is never drawn)
+//   rlcard/games/limitholdem/utils.py:3-614    7-card ranking (== standard poker order; bitmask evaluator below)
+//   rlcard/envs/limitholdem.py:40-96           obs[72] (card bits + 52 + 5*round + raises) and the id fallback
+// Shuffle: Fisher-Yates fixes position i at step i, and only deck[43..51] is ever dealt, so the first nine swaps are
+// tracked in registers (a 9-entry position map) and the remaining 42 steps only consume their random_interval draws.
+// Packed state, 4 u32 words per env (word-major [4][N]):
+//   w0: hole cards p0c0:6 p0c1:6 p1c0:6 p1c1:6 in0:6 (bits 24..29) ptr:1 (30) over:1 (31)
+//   w1: board c0..c4 6 bits each (0..29)
+//   w2: in1:6 r0:5 r1:5 have_raised:3 not_raise_num:2 rc:3 f0:1 f1:1 use_prev:1 (bits 0..26)
+//   w3: raise_nums 4x3 (0..11), prev_raise_nums 4x3 (12..23)
+#pragma once
+#include "cs_device.h"
+
+namespace cs {
+
+__device__ __forceinline__ int top_bit(uint32_t m) { return 31 - __builtin_clz(m); }
+
+// highest straight top rank (2=0 .. A=12) in a 13-bit rank mask, -1 if none; the wheel tops at 5 (= 3)
+__device__ __forceinline__ int top_straight13(uint32_t mask)
+{
+    const uint32_t m = (mask << 1) | ((mask >> 12) & 1u);
+    const uint32_t x = m & (m >> 1) & (m >> 2) & (m >> 3) & (m >> 4);
+    return x ? top_bit(x) + 3 : -1;
+}
+
+// 7-card hand value; larger = better, equal = split. cat << 20 | five 4-bit tiebreak ranks
+__device__ inline uint32_t holdem_rank7(const int (&c)[7])
+{
+    uint64_t cnt = 0;          // 13 nibbles: count per rank
+    uint32_t sm[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+        const int s = c[k] / 13, q = c[k] - 13 * s, r = q == 0 ? 12 : q - 1;
+        cnt += 1ull << (4 * r);
+        const uint32_t b = 1u << r;
+        sm[0] |= s == 0 ? b : 0u; sm[1] |= s == 1 ? b : 0u; sm[2] |= s == 2 ? b : 0u; sm[3] |= s == 3 ? b : 0u;
+    }
+    uint32_t m1 = 0, m2 = 0, m3 = 0, m4 = 0;
+#pragma unroll
+    for (int r = 0; r < 13; r++) {
+        const uint32_t n = (uint32_t)(cnt >> (4 * r)) & 15u;
+        m1 |= (n == 1u) << r; m2 |= (n == 2u) << r; m3 |= (n == 3u) << r; m4 |= (n == 4u) << r;
+    }
+    const uint32_t all = m1 | m2 | m3 | m4;
+    uint32_t fm = 0;
+#pragma unroll
+    for (int s = 0; s < 4; s++) fm = __popc(sm[s]) >= 5 ? sm[s] : fm;
+    uint32_t cat, v0 = 0, v1 = 0, v2 = 0, v3 = 0, v4 = 0;
+    const int sf = fm ? top_straight13(fm) : -1;
+    if (sf >= 0) {
+        cat = 9; v0 = sf;
+    } else if (m4) {
+        cat = 8; v0 = top_bit(m4); v1 = top_bit(all & ~(1u << v0));
+    } else if (m3 && (__popc(m3) >= 2 || m2)) {
+        cat = 7; v0 = top_bit(m3); v1 = top_bit((m3 & ~(1u << v0)) | m2);
+    } else if (fm) {
+        cat = 6;
+        uint32_t f = fm;
+        v0 = top_bit(f); f &= ~(1u << v0); v1 = top_bit(f); f &= ~(1u << v1); v2 = top_bit(f); f &= ~(1u << v2);
+        v3 = top_bit(f); f &= ~(1u << v3); v4 = top_bit(f);
+    } else if (top_straight13(all) >= 0) {
+        cat = 5; v0 = top_straight13(all);
+    } else if (m3) {
+        cat = 4; v0 = top_bit(m3);
+        uint32_t k = m1;
+        v1 = top_bit(k); k &= ~(1u << v1); v2 = top_bit(k);
+    } else if (__popc(m2) >= 2) {
+        cat = 3;
+        uint32_t p = m2;
+        v0 = top_bit(p); p &= ~(1u << v0); v1 = top_bit(p);
+        v2 = top_bit(all & ~(1u << v0) & ~(1u << v1));
+    } else if (m2) {
+        cat = 2; v0 = top_bit(m2);
+        uint32_t k = m1;
+        v1 = top_bit(k); k &= ~(1u << v1); v2 = top_bit(k); k &= ~(1u << v2); v3 = top_bit(k);
+    } else {
+        cat = 1;
+        uint32_t k = m1;
+        v0 = top_bit(k); k &= ~(1u << v0); v1 = top_bit(k); k &= ~(1u << v1); v2 = top_bit(k); k &= ~(1u << v2);
+        v3 = top_bit(k); k &= ~(1u << v3); v4 = top_bit(k);
+    }
+    return cat << 20 | v0 << 16 | v1 << 12 | v2 << 8 | v3 << 4 | v4;
+}
+
+struct Limit {
+    static constexpr int OBS = 72, A = 4, P = 2, LB = 1, WORDS = 4, ACTION_BYTES = 1;
+    static constexpr int NB = 3;
+    static constexpr bool RAW_OBS = false;
+    static constexpr int SCRATCH_WORDS = 0;
+    __device__ __forceinline__ void bind(uint32_t*, const GameParams&) {}
+    enum { CALL = 0, RAISE = 1, FOLD = 2, CHECK = 3 };
+
+    uint32_t w0, w1, w2, w3;
+
+    // field accessors on the packed words (kept packed in registers: few live values, cheap bitfield ops)
+    __device__ __forceinline__ int hole(int p, int k) const { return (w0 >> (6 * (2 * p + k))) & 63; }
+    __device__ __forceinline__ int board(int k) const { return (w1 >> (6 * k)) & 63; }
+    __device__ __forceinline__ int in0() const { return (w0 >> 24) & 63; }
+    __device__ __forceinline__ int in1() const { return w2 & 63; }
+    __device__ __forceinline__ int r0() const { return (w2 >> 6) & 31; }
+    __device__ __forceinline__ int r1() const { return (w2 >> 11) & 31; }
+    __device__ __forceinline__ int hr() const { return (w2 >> 16) & 7; }
+    __device__ __forceinline__ int nrn() const { return (w2 >> 19) & 3; }
+    __device__ __forceinline__ int rc() const { return (w2 >> 21) & 7; }
+    __device__ __forceinline__ int f0() const { return (w2 >> 24) & 1; }
+    __device__ __forceinline__ int f1() const { return (w2 >> 25) & 1; }
+    __device__ __forceinline__ int use_prev() const { return (w2 >> 26) & 1; }
+    __device__ __forceinline__ int ptr() const { return (w0 >> 30) & 1; }
+
+    __device__ __forceinline__ void load(const uint32_t* st, int64_t n, int64_t env)
+    {
+        w0 = st[env]; w1 = st[n + env]; w2 = st[2 * n + env]; w3 = st[3 * n + env];
+    }
+    __device__ __forceinline__ void store(uint32_t* st, int64_t n, int64_t env) const
+    {
+        st[env] = w0; st[n + env] = w1; st[2 * n + env] = w2; st[3 * n + env] = w3;
+    }
+    __device__ __forceinline__ void blank() { w0 = 1u << 31; w1 = 0; w2 = 0; w3 = 0; }
+
+    __device__ __forceinline__ int current() const { return ptr(); }
+    __device__ __forceinline__ bool is_over() const { return (w0 >> 31) != 0; }
+
+    __device__ __forceinline__ uint32_t legal() const
+    {
+        const int a = r0(), b = r1(), mx = a > b ? a : b, rp = ptr() ? b : a;
+        uint32_t m = 0xF;
+        if (hr() >= 4) m &= ~(1u << RAISE);
+        if (rp < mx) m &= ~(1u << CHECK);
+        if (rp == mx) m &= ~(1u << CALL);
+        return m;
+    }
+
+    __device__ __forceinline__ void observe(int player, uint32_t (&bits)[NB]) const
+    {
+        bits[0] = bits[1] = bits[2] = 0;
+        const int r = rc(), npub = r == 0 ? 0 : (r == 1 ? 3 : (r == 2 ? 4 : 5));
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+            if (k < npub) set_bit(bits, board(k));
+        set_bit(bits, hole(player, 0));
+        set_bit(bits, hole(player, 1));
+        const uint32_t rn = use_prev() ? (w3 >> 12) : w3;
+#pragma unroll
+        for (int i = 0; i < 4; i++) set_bit(bits, 52 + 5 * i + (int)((rn >> (3 * i)) & 7u));
+    }
+
+    __device__ __forceinline__ void reset(MtLane& rng)
+    {
+        int J[9], V[9], D[9];
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            const int i = 51 - k;
+            const int j = (int)rng.interval((uint32_t)i);
+            int vi = i, vj = j;
+#pragma unroll
+            for (int q = 0; q < k; q++) {   // oldest -> newest: the newest write to a position wins
+                vi = J[q] == i ? V[q] : vi;
+                vj = J[q] == j ? V[q] : vj;
+            }
+            D[k] = vj;
+            J[k] = j;
+            V[k] = vi;
+        }
+        for (int i = 42; i >= 1; i--) (void)rng.interval((uint32_t)i);
+        // hole i -> player i%2, card i/2, from deck[51-i] = D[i]
+        const int s = (int)rng.interval(1u);
+        const int in_0 = s == 0 ? 1 : 2, in_1 = s == 0 ? 2 : 1;
+        const int first = s;  // (BB + 1) % 2 with BB = (s + 1) % 2
+        w0 = (uint32_t)D[0] | (uint32_t)D[2] << 6 | (uint32_t)D[1] << 12 | (uint32_t)D[3] << 18 |
+             (uint32_t)in_0 << 24 | (uint32_t)first << 30;
+        w1 = (uint32_t)D[4] | (uint32_t)D[5] << 6 | (uint32_t)D[6] << 12 | (uint32_t)D[7] << 18 |
+             (uint32_t)D[8] << 24;
+        w2 = (uint32_t)in_1 | (uint32_t)in_0 << 6 | (uint32_t)in_1 << 11 | 1u << 26;  // raised = in_chips, use_prev
+        w3 = (w3 & 0xFFFu) << 12;                                                      // prev <- current, current <- 0
+    }
+
+    __device__ __forceinline__ void step(int a, MtLane&)
+    {
+        const uint32_t lg = legal();
+        if (a < 0 || a > 3 || !((lg >> a) & 1u)) a = ((lg >> CHECK) & 1u) ? CHECK : FOLD;
+        int i0 = in0(), i1 = in1(), ra0 = r0(), ra1 = r1(), h = hr(), nr = nrn(), r = rc(), p = ptr();
+        int fo0 = f0(), fo1 = f1();
+        const int mx = ra0 > ra1 ? ra0 : ra1, rp = p ? ra1 : ra0, amt = r >= 2 ? 4 : 2;
+        int add = 0, nraised = rp;
+        if (a == CALL) { add = mx - rp; nraised = mx; nr += 1; }
+        else if (a == RAISE) { add = mx - rp + amt; nraised = mx + amt; h += 1; nr = 1; }
+        else if (a == FOLD) { if (p) fo1 = 1; else fo0 = 1; }
+        else { nr += 1; }
+        if (p) { i1 += add; ra1 = nraised; } else { i0 += add; ra0 = nraised; }
+        p ^= 1;
+        if (p ? fo1 : fo0) p ^= 1;
+        w3 = (w3 & ~(7u << (3 * r))) | ((uint32_t)h << (3 * r));   // history_raise_nums[round] = have_raised
+        if (nr >= 2) {
+            r += 1;
+            h = 0; nr = 0; ra0 = 0; ra1 = 0;
+        }
+        const int over = (fo0 + fo1 == 1) || r >= 4;
+        w0 = (w0 & 0x00FFFFFFu) | (uint32_t)i0 << 24 | (uint32_t)p << 30 | (uint32_t)over << 31;
+        w2 = (uint32_t)i1 | (uint32_t)ra0 << 6 | (uint32_t)ra1 << 11 | (uint32_t)h << 16 | (uint32_t)nr << 19 |
+             (uint32_t)r << 21 | (uint32_t)fo0 << 24 | (uint32_t)fo1 << 25;   // use_prev cleared
+    }
+
+    __device__ __forceinline__ void payoffs(float (&out)[P]) const
+    {
+        int win0, win1;
+        if (f0() || f1()) {
+            win0 = !f0(); win1 = !f1();
+        } else {
+            int c0[7] = {hole(0, 0), hole(0, 1), board(0), board(1), board(2), board(3), board(4)};
+            int c1[7] = {hole(1, 0), hole(1, 1), board(0), board(1), board(2), board(3), board(4)};
+            const uint32_t v0 = holdem_rank7(c0), v1 = holdem_rank7(c1);
+            win0 = v0 >= v1; win1 = v1 >= v0;
+        }
+        const int a = in0(), b = in1(), m = a < b ? a : b;
+        float p0 = 0.f, p1 = 0.f;
+        if (!(win0 && win1)) {
+            p0 = win0 ? (float)m : -(float)m;
+            p1 = -p0;
+        }
+        out[0] = p0 * 0.5f;
+        out[1] = p1 * 0.5f;
+    }
+};
+
+}  // namespace cs

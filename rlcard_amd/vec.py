@@ -1,0 +1,162 @@
+"""Batched lockstep envs on one GPU: the hot path behind rlcard_amd.make() and bench.py.
+
+A VecEnv holds `num_envs` independent games of one kind in HBM (one C-ABI handle, include/cardsim.h). Outputs are
+torch tensors on the env's device, written by the HIP kernels on the current torch stream:
+
+  obs    uint8   [N, obs_dim]      Env._extract_state(...)['obs'] of the current player (0/1 values; blackjack scores)
+  legal  uint8   [N, legal_bytes]  legal action ids as a little-endian bitmask (see legal_mask())
+  player uint8   [N]               Env.get_player_id()
+  reward float32 [N, num_players]  Env.get_payoffs() on the step that ends a game, else 0
+  done   uint8   [N]               Env.is_over()
+
+Env i is seeded with seeds[i] (default: seed + env_base + i) exactly as rlcard.make(..., config={'seed': s}) seeds
+its numpy RandomState, so env i replays the reference's deals for that seed.
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _abi
+from .seeding import seed_keys
+
+__all__ = ['VecEnv', 'legal_mask', 'legal_ids']
+
+
+def legal_mask(legal_bytes, num_actions):
+    """uint8 [..., legal_bytes] bitmask -> bool [..., num_actions]."""
+    bits = torch.arange(8, device=legal_bytes.device, dtype=torch.uint8)
+    m = (legal_bytes.unsqueeze(-1) >> bits) & 1
+    return m.reshape(*legal_bytes.shape[:-1], -1)[..., :num_actions].bool()
+
+
+def legal_ids(legal_row):
+    """One env's bitmask (1-d uint8, any device) -> sorted list of legal action ids."""
+    b = np.unpackbits(np.asarray(legal_row.cpu() if torch.is_tensor(legal_row) else legal_row, dtype=np.uint8),
+                      bitorder='little')
+    return [int(i) for i in np.nonzero(b)[0]]
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+class VecEnv:
+    def __init__(self, env_id, num_envs, seed=0, seeds=None, device=None, config=None, env_base=0):
+        config = dict(config or {})
+        self.env_id = env_id
+        if env_id not in _abi.GAME_IDS:
+            raise ValueError('Cannot find env_id: {}'.format(env_id))
+        self.game = _abi.GAME_IDS[env_id]
+        self.num_envs = int(num_envs)
+        self.env_base = int(env_base)
+        if device is None:
+            device = torch.cuda.current_device() if torch.cuda.is_available() else 0
+        self.device = torch.device('cuda', device) if isinstance(device, int) else torch.device(device)
+        if self.device.type != 'cuda':
+            raise _abi.CardsimError('VecEnv runs on the GPU only (got device %s)' % self.device)
+        np_ = int(config.get('game_num_players', 0))
+        nd = int(config.get('game_num_decks', -1))
+        self.info, self.cfg = _abi.game_info(self.game, np_, nd)
+        self.obs_dim = self.info.obs_dim
+        self.num_actions = self.info.num_actions
+        self.num_players = self.info.num_players
+        self.legal_bytes = self.info.legal_bytes
+        self.action_dtype = torch.uint8 if self.info.action_bytes == 1 else torch.int16
+        L = _abi.lib()
+        h = C.c_void_p()
+        _abi.check(L.cs_create(C.byref(h), self.game, self.num_envs, self.device.index or 0, C.byref(self.cfg)),
+                   'cs_create')
+        self._h = h
+        if seeds is None:
+            seeds = range(int(seed) + self.env_base, int(seed) + self.env_base + self.num_envs)
+        self.seed(seeds)
+
+    # -- lifetime ----------------------------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, '_h', None) is not None and self._h.value:
+            _abi.lib().cs_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # -- API -----------------------------------------------------------------------------------------------------
+    def seed(self, seeds, first_env=0):
+        keys, lens = seed_keys(seeds)
+        n = len(lens)
+        with torch.cuda.device(self.device):
+            _abi.check(_abi.lib().cs_seed(self._h, keys.ctypes.data_as(C.c_void_p), lens.ctypes.data_as(C.c_void_p),
+                                          first_env, n, self._stream()), 'cs_seed')
+
+    def new_step_out(self, lead=()):
+        n, d = self.num_envs, self.device
+        return dict(obs=torch.empty(lead + (n, self.obs_dim), dtype=torch.uint8, device=d),
+                    legal=torch.empty(lead + (n, self.legal_bytes), dtype=torch.uint8, device=d),
+                    player=torch.empty(lead + (n,), dtype=torch.uint8, device=d),
+                    reward=torch.empty(lead + (n, self.num_players), dtype=torch.float32, device=d),
+                    done=torch.empty(lead + (n,), dtype=torch.uint8, device=d))
+
+    @staticmethod
+    def _step_struct(o):
+        return _abi.StepOut(_ptr(o.get('obs')), _ptr(o.get('legal')), _ptr(o.get('player')), _ptr(o.get('reward')),
+                            _ptr(o.get('done')))
+
+    def reset(self, out=None):
+        o = out if out is not None else self.new_step_out()
+        with torch.cuda.device(self.device):
+            _abi.check(_abi.lib().cs_reset(self._h, C.byref(self._step_struct(o)), self._stream()), 'cs_reset')
+        return o
+
+    def step(self, actions, out=None):
+        a = torch.as_tensor(actions, device=self.device).to(torch.int32).contiguous()
+        if a.numel() != self.num_envs:
+            raise ValueError('expected %d actions, got %d' % (self.num_envs, a.numel()))
+        o = out if out is not None else self.new_step_out()
+        with torch.cuda.device(self.device):
+            _abi.check(_abi.lib().cs_step(self._h, _ptr(a), C.byref(self._step_struct(o)), self._stream()),
+                       'cs_step')
+        return o
+
+    def observe(self, player, out=None):
+        o = out if out is not None else self.new_step_out()
+        o = {k: o[k] for k in ('obs', 'legal', 'player', 'done')}
+        with torch.cuda.device(self.device):
+            _abi.check(_abi.lib().cs_observe(self._h, int(player), C.byref(self._step_struct(o)), self._stream()),
+                       'cs_observe')
+        return o
+
+    def new_traj_out(self, T):
+        o = self.new_step_out((T,))
+        o['action'] = torch.empty((T, self.num_envs), dtype=self.action_dtype, device=self.device)
+        return o
+
+    def rollout(self, T, policy_seed=0, t0=0, out=None):
+        """T lockstep steps of the uniform-random legal policy, auto-reset; -> trajectory dict of [T, N, ...]."""
+        o = out if out is not None else self.new_traj_out(T)
+        s = _abi.TrajOut(_ptr(o['obs']), _ptr(o['legal']), _ptr(o['player']), _ptr(o['action']),
+                         _ptr(o['reward']), _ptr(o['done']))
+        with torch.cuda.device(self.device):
+            _abi.check(_abi.lib().cs_rollout(self._h, int(T), int(policy_seed) & (2 ** 64 - 1), int(t0),
+                                             self.env_base, C.byref(s), self._stream()), 'cs_rollout')
+        return o
+
+    # -- introspection (synchronous) ------------------------------------------------------------------------------
+    def env_state_words(self, env):
+        buf = (C.c_uint32 * self.info.state_words)()
+        _abi.check(_abi.lib().cs_get_env_state(self._h, int(env), buf, self.info.state_words), 'cs_get_env_state')
+        return list(buf)
+
+    def rng_position(self, env):
+        v = C.c_uint32()
+        _abi.check(_abi.lib().cs_get_rng_ctl(self._h, int(env), C.byref(v)), 'cs_get_rng_ctl')
+        return v.value & 0x7FF
+
+    def set_serial_refill(self, enable):
+        _abi.check(_abi.lib().cs_debug_set_serial_refill(self._h, 1 if enable else 0), 'cs_debug_set_serial_refill')

@@ -1,0 +1,49 @@
+"""CPU-side checks of the C ABI boundary: the in-tree library loads and exports every symbol include/cardsim.h
+declares; calls fail loudly (no CPU fallback) without a GPU."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from rlcard_amd import _abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, 'include', 'cardsim.h')).read()
+    return sorted(set(re.findall(r'\b(cs_[a-z_]+)\s*\(', src)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _abi.lib()
+    declared = header_symbols()
+    assert set(declared) == set(_abi.SYMBOLS)
+    for s in declared:
+        assert hasattr(L, s), s
+
+
+def test_game_info_shapes():
+    shapes = {'leduc-holdem': (36, 4, 2, 1), 'limit-holdem': (72, 4, 2, 1), 'blackjack': (2, 2, 1, 1)}
+    for game, (o, a, p, lb) in shapes.items():
+        info, _ = _abi.game_info(game)
+        assert (info.obs_dim, info.num_actions, info.num_players, info.legal_bytes) == (o, a, p, lb)
+
+
+def test_create_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip('GPU present')
+    h = C.c_void_p()
+    cfg = _abi.Config(0, -1)
+    rc = _abi.lib().cs_create(C.byref(h), 1, 64, 0, C.byref(cfg))
+    assert rc == -2 and b'GPU' in _abi.lib().cs_last_error()
+    with pytest.raises(_abi.CardsimError):
+        _abi.check(rc, 'cs_create')
+
+
+def test_invalid_arguments_are_rejected():
+    info = _abi.GameInfo()
+    assert _abi.lib().cs_game_info_get(9, None, C.byref(info)) == -4
+    assert _abi.lib().cs_create(None, 1, 64, 0, None) == -1

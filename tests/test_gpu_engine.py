@@ -1,0 +1,166 @@
+"""HIP engine vs the reference (golden streams) and vs the CPU oracle, through the C ABI. Needs a GPU."""
+import numpy as np
+import pytest
+
+import golden_replay as gr
+from rlcard_amd import seeding
+
+torch = pytest.importorskip('torch')
+pytestmark = pytest.mark.gpu
+
+GAMES = [('leduc-holdem', 'leduc'), ('limit-holdem', 'limit'), ('blackjack', 'blackjack')]
+
+
+def _np(o):
+    return {k: v.cpu().numpy() for k, v in o.items()}
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail('GPU tests need a visible GPU (run them on the MI355X box)')
+
+
+def _vec(game, n, **kw):
+    from rlcard_amd import VecEnv
+    return VecEnv(game, n, **kw)
+
+
+@pytest.mark.parametrize('game,name', GAMES)
+def test_single_env_replays_reference_stream(game, name):
+    d = gr.load(name)
+
+    class One:
+        def __init__(self, seed):
+            self.v = _vec(game, 1, seeds=[seed])
+
+        def reset(self):
+            return {k: x[0] for k, x in _np(self.v.reset()).items()}
+
+        def step(self, a):
+            return {k: x[0] for k, x in _np(self.v.step([a])).items()}
+
+        def observe(self, p):
+            o = _np(self.v.observe(p))
+            return o['obs'][0], o['legal'][0]
+
+    num_actions = _vec(game, 1).num_actions
+    assert gr.replay(d, lambda ei, s: One(s), num_actions) == len(d['ev_kind'])
+
+
+@pytest.mark.parametrize('game,name', GAMES)
+def test_batched_replay_with_lazy_reset(game, name):
+    """All fixture seeds as one batch; a 'reset' event after a finished game is a step with any action (lazy reset)."""
+    d = gr.load(name)
+    seeds = [int(s) for s in d['seeds']]
+    v = _vec(game, len(seeds), seeds=seeds)
+    per_env = [np.nonzero(d['ev_env'] == i)[0] for i in range(len(seeds))]
+    ticks = max(len(x) for x in per_env)
+    out = _np(v.reset())
+    for tick in range(ticks):
+        if tick > 0:
+            acts = np.zeros(len(seeds), np.int32)
+            for i, ev in enumerate(per_env):
+                if tick < len(ev) and d['ev_kind'][ev[tick]] == 1:
+                    acts[i] = d['ev_act'][ev[tick]]
+            out = _np(v.step(torch.from_numpy(acts).cuda()))
+        for i, ev in enumerate(per_env):
+            if tick >= len(ev):
+                continue
+            k = ev[tick]
+            n = int(d['ev_obs_len'][k])
+            assert np.array_equal(out['obs'][i][:n], d['ev_obs'][k][:n]), (i, tick)
+            assert np.array_equal(out['legal'][i], gr.legal_bits_of(d, k, v.num_actions)), (i, tick)
+            assert out['player'][i] == d['ev_player'][k] and out['done'][i] == d['ev_done'][k], (i, tick)
+            if d['ev_done'][k]:
+                assert np.array_equal(out['reward'][i].astype(np.float64), d['ev_payoff'][k]), (i, tick)
+
+
+def _oracle_batch(oracle, game, seeds):
+    keys, lens = seeding.seed_keys(seeds)
+    return oracle.Batch(game, len(seeds), keys, lens)
+
+
+def _assert_same(got, exp, what):
+    for k in exp:
+        if k not in got:
+            continue
+        g, e = got[k], exp[k]
+        if g.dtype != e.dtype:
+            e = e.astype(g.dtype)
+        if not np.array_equal(g, e):
+            bad = np.argwhere(g != e)
+            raise AssertionError('%s: %s differs at %d places, first %s: got %s expected %s'
+                                 % (what, k, len(bad), bad[0], g[tuple(bad[0])], e[tuple(bad[0])]))
+
+
+@pytest.mark.parametrize('game,name', GAMES)
+def test_step_api_matches_oracle(oracle, game, name):
+    n = 3000  # not a multiple of 64: exercises the tail wave
+    seeds = list(range(100, 100 + n))
+    v = _vec(game, n, seed=100)
+    ob = _oracle_batch(oracle, game, seeds)
+    rng = np.random.RandomState(0)
+    _assert_same(_np(v.reset()), ob.reset(), 'reset')
+    for t in range(120):
+        acts = rng.randint(-1, v.num_actions + 1, size=n).astype(np.int32)   # includes illegal ids
+        _assert_same(_np(v.step(torch.from_numpy(acts).cuda())), ob.step(acts), 'step %d' % t)
+    for p in range(v.num_players):
+        o = _np(v.observe(p))
+        for i in (0, 1, n // 2, n - 1):
+            obs, legal = ob.observe(i, p)
+            assert np.array_equal(o['obs'][i], obs) and np.array_equal(o['legal'][i], legal)
+
+
+@pytest.mark.parametrize('serial', [False, True])
+@pytest.mark.parametrize('game,name', GAMES)
+def test_rollout_matches_oracle(oracle, game, name, serial):
+    n, T = 4160 + 37, 48
+    seeds = list(range(7, 7 + n))
+    v = _vec(game, n, seed=7)
+    v.set_serial_refill(serial)
+    ob = _oracle_batch(oracle, game, seeds)
+    v.reset()
+    ob.reset()
+    for chunk in range(3):   # state, RNG position and policy counter carry across launches
+        got = _np(v.rollout(T, policy_seed=99, t0=chunk * T))
+        exp = ob.rollout(T, 99, chunk * T, 0)
+        _assert_same(got, exp, 'rollout chunk %d' % chunk)
+    torch.cuda.synchronize()
+    for i in (0, 63, 64, 2000, n - 1):
+        assert v.rng_position(i) == ob.draws(i) % 1248
+
+
+@pytest.mark.parametrize('game,name', GAMES)
+def test_full_size_rollout_properties_and_sampled_parity(oracle, game, name):
+    n = {'leduc-holdem': 1 << 20, 'limit-holdem': 262144, 'blackjack': 262144}[game]
+    T = 16
+    v = _vec(game, n, seed=42)
+    v.reset()
+    tr = v.rollout(T, policy_seed=5)
+    torch.cuda.synchronize()
+    from rlcard_amd import legal_mask
+    lm = legal_mask(tr['legal'], v.num_actions)                       # [T, N, A]
+    a = tr['action'].long()
+    assert bool((lm.sum(-1) > 0).all()), 'every acting state has a legal action'
+    assert bool(lm.gather(-1, a.unsqueeze(-1)).all()), 'policy picks legal actions'
+    done = tr['done'].bool()
+    rsum = tr['reward'].sum(-1)
+    if game == 'blackjack':   # player vs dealer: payoff in {-1, 0, 1}, not zero-sum
+        assert bool(((tr['reward'][done] == -1) | (tr['reward'][done] == 0) | (tr['reward'][done] == 1)).all())
+        assert bool((tr['obs'][..., 0] >= 4).all()) and bool((tr['obs'][..., 0] <= 21).all()), 'acting player not bust'
+    else:
+        assert bool((rsum[done].abs() < 1e-6).all()), 'zero-sum payoffs'
+    assert bool((tr['reward'][~done] == 0).all())
+    if game == 'leduc-holdem':
+        assert bool((tr['obs'].sum(-1) >= 3).all())
+    if game == 'limit-holdem':
+        s = tr['obs'].long().sum(-1)
+        assert bool(((s >= 6) & (s <= 11)).all()), 'limit obs: 2 hole + 0/3/4/5 board + 4 raise slots'
+    # exact parity on three 384-env windows (start, middle, end) replayed by the oracle with the same env ids
+    for start in (0, n // 2 + 17, n - 384):
+        ob = _oracle_batch(oracle, game, range(42 + start, 42 + start + 384))
+        ob.reset()
+        exp = ob.rollout(T, 5, 0, start)
+        got = {k: x[:, start:start + 384].cpu().numpy() for k, x in tr.items()}
+        _assert_same(got, exp, 'window %d' % start)
