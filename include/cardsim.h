@@ -122,6 +122,10 @@ int cs_get_rng_ctl(cs_handle* h, int64_t env, uint32_t* host_ctl);
  * serial twist; results must be identical. */
 int cs_debug_set_serial_refill(cs_handle* h, int32_t enable);
 
+/* Tuning hook: kernel variant bits (bit 0 = serial MT refill, bit 1 = reserved, bit 2 = dword instead of 16-B obs
+ * stores). Results are identical for every value. */
+int cs_debug_set_kernel_flags(cs_handle* h, int32_t flags);
+
 const char* cs_last_error(void);
 const char* cs_version(void);
 

@@ -6,7 +6,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libcardsim.so')
+LIB_PATH = os.path.join(_HERE, os.environ.get('CARDSIM_LIB', 'libcardsim.so'))   # CARDSIM_LIB: A/B builds only
 
 GAME_IDS = {'blackjack': 0, 'leduc-holdem': 1, 'limit-holdem': 2, 'doudizhu': 3}
 
@@ -36,8 +36,8 @@ class TrajOut(C.Structure):
 
 # every symbol include/cardsim.h declares (tests check the library exports all of them)
 SYMBOLS = ('cs_game_info_get', 'cs_create', 'cs_destroy', 'cs_seed', 'cs_reset', 'cs_step', 'cs_observe',
-           'cs_rollout', 'cs_get_env_state', 'cs_get_rng_ctl', 'cs_debug_set_serial_refill', 'cs_last_error',
-           'cs_version')
+           'cs_rollout', 'cs_get_env_state', 'cs_get_rng_ctl', 'cs_debug_set_serial_refill', 'cs_debug_set_kernel_flags',
+           'cs_last_error', 'cs_version')
 
 _lib = None
 
@@ -67,10 +67,11 @@ def lib():
     L.cs_get_env_state.argtypes = [vp, i64, vp, i32]
     L.cs_get_rng_ctl.argtypes = [vp, i64, vp]
     L.cs_debug_set_serial_refill.argtypes = [vp, i32]
+    L.cs_debug_set_kernel_flags.argtypes = [vp, i32]
     L.cs_last_error.restype = C.c_char_p
     L.cs_version.restype = C.c_char_p
     for name in ('cs_game_info_get', 'cs_create', 'cs_seed', 'cs_reset', 'cs_step', 'cs_observe', 'cs_rollout',
-                 'cs_get_env_state', 'cs_get_rng_ctl', 'cs_debug_set_serial_refill'):
+                 'cs_get_env_state', 'cs_get_rng_ctl', 'cs_debug_set_serial_refill', 'cs_debug_set_kernel_flags'):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

@@ -81,6 +81,15 @@ int cs_create(cs_handle** out, int32_t game, int64_t num_envs, int32_t device, c
         cs_destroy(h);
         return fail_hip(e, "hipMalloc (env state)");
     }
+    const int64_t sb = cs::stage_bytes_per_env(game, info.num_players);
+    if (sb > 0) {   // rollout staging rows, whole waves (the copy moves 16-B chunks of full rows)
+        const size_t rows = (n + 63) / 64 * 64;
+        if ((e = hipMalloc((void**)&h->b.sctl, n * sizeof(uint32_t))) != hipSuccess ||
+            (e = hipMalloc((void**)&h->b.sbuf, rows * (size_t)sb)) != hipSuccess) {
+            cs_destroy(h);
+            return fail_hip(e, "hipMalloc (rollout staging)");
+        }
+    }
     *out = h;
     return CS_OK;
 }
@@ -92,6 +101,8 @@ void cs_destroy(cs_handle* h)
     if (h->b.mt) (void)hipFree(h->b.mt);
     if (h->b.ctl) (void)hipFree(h->b.ctl);
     if (h->b.state) (void)hipFree(h->b.state);
+    if (h->b.sctl) (void)hipFree(h->b.sctl);
+    if (h->b.sbuf) (void)hipFree(h->b.sbuf);
     delete h;
 }
 
@@ -196,7 +207,15 @@ int cs_get_rng_ctl(cs_handle* h, int64_t env, uint32_t* host_ctl)
 int cs_debug_set_serial_refill(cs_handle* h, int32_t enable)
 {
     if (!h) return fail(CS_E_INVALID, "null argument");
-    h->b.serial_refill = enable ? 1 : 0;
+    h->b.serial_refill = (h->b.serial_refill & ~1) | (enable ? 1 : 0);
+    return CS_OK;
+}
+
+int cs_debug_set_kernel_flags(cs_handle* h, int32_t flags)
+{
+    if (!h) return fail(CS_E_INVALID, "null argument");
+    if (flags < 0 || flags > 7) return fail(CS_E_INVALID, "unknown kernel flag bits");
+    h->b.serial_refill = flags;
     return CS_OK;
 }
 

@@ -30,6 +30,7 @@ struct Blackjack {
     static constexpr int NB = 1;               // raw obs dwords
     static constexpr bool RAW_OBS = true;      // observe() returns byte values, not a 0/1 bitmap
     static constexpr int SCRATCH_WORDS = WORDS;
+    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_R = 100;  // MT staging (see MtLaneT)
     static constexpr int HAND_CAP = 12;
 
     uint32_t* s;   // lane scratch: word i at s[i * WAVE]
@@ -91,7 +92,8 @@ struct Blackjack {
         return sc;
     }
 
-    __device__ __forceinline__ void deal(MtLane& rng, int h)
+    template <class Rng>
+    __device__ __forceinline__ void deal(Rng& rng, int h)
     {
         const int len = (W(14) >> 20) & 63;
         const int idx = (int)rng.interval((uint32_t)(len - 1));
@@ -118,7 +120,8 @@ struct Blackjack {
         raw[0] = (uint32_t)mine | (uint32_t)dealer << 8;
     }
 
-    __device__ __forceinline__ void reset(MtLane& rng)
+    template <class Rng>
+    __device__ __forceinline__ void reset(Rng& rng)
     {
         // 52-card Fisher-Yates in the deck words (bytes), then the initial deal
 #pragma unroll
@@ -140,7 +143,8 @@ struct Blackjack {
         }
     }
 
-    __device__ __forceinline__ void finish(MtLane& rng)
+    template <class Rng>
+    __device__ __forceinline__ void finish(Rng& rng)
     {
         while (score(NP, 0) < 17) deal(rng, NP);
         const int d = score(NP, 0);
@@ -159,7 +163,8 @@ struct Blackjack {
         W(14) = (W(14) & ~(7u << 26)) | 1u << 29;   // game_pointer = 0, over
     }
 
-    __device__ __forceinline__ void step(int a, MtLane& rng)
+    template <class Rng>
+    __device__ __forceinline__ void step(int a, Rng& rng)
     {
         const int gp = current();
         bool advance = true;

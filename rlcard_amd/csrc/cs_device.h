@@ -89,15 +89,52 @@ __device__ __forceinline__ void mt_twist_wave(const uint32_t* __restrict__ src, 
     }
 }
 
-// One lane's view of its env's stream.
-struct MtLane {
+// 64-bit pointer held by lane j (readlane returns int: go through uint32_t so bit 31 of the low half is not
+// sign-extended into the high half)
+__device__ __forceinline__ uint32_t* lane_ptr(uint32_t* p, int j)
+{
+    const uint64_t b = (uint64_t)(uintptr_t)p;
+    const uint64_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, j);
+    const uint64_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), j);
+    return (uint32_t*)(uintptr_t)(lo | (hi << 32));
+}
+
+// One lane's view of its env's stream. MODE selects how draws are served:
+//   STAGE_NONE  one global load per draw (single-step kernels: staging would cost more than it saves);
+//   STAGE_REGS  16 staged bytes in 4 VGPRs (Leduc: a reset needs ~7 draws);
+//   STAGE_LDS   W staged bytes in a per-lane LDS row (Limit / Blackjack: a reset needs ~72-80 draws).
+// Why staging: lanes sit at different stream positions, so one load per draw is a 64-line gather per wave
+// instruction, and a reset's rejection loops issue one such gather per trip of the slowest lane (rocprofv3 on
+// k_rollout<Leduc>: TA busy 68% of the kernel, ~300 L1 accesses per wave-step, waves waiting 80% of their cycles).
+// Every draw of this engine is random_interval(max <= 53), which looks only at the low 8 bits of the tempered word,
+// so at step boundaries (after the refill: both blocks valid) lanes running low restage their next words, temper
+// them and keep the low bytes; draws then read registers / LDS, global only as a fallback when a lane outruns its
+// stage. Measured on MI355X (tools/ab_rollout.py): a per-draw 8-word register window was 1.6x slower and 8/16-word
+// register bursts inside the reset +3% / 2.7x slower than one load per draw.
+enum { STAGE_NONE = 0, STAGE_REGS = 1, STAGE_LDS = 2 };
+
+template <int MODE = STAGE_NONE>
+struct MtLaneT {
     uint32_t* base;  // mt + env * MT_WORDS
     uint32_t pos;
     uint32_t stale;
+    uint32_t sp, sn;            // stream position of staged byte 0; staged bytes
+    uint32_t s0, s1, s2, s3;    // STAGE_REGS: 16 staged bytes
+    const uint8_t* stg;         // STAGE_LDS: this lane's row
 
-    __device__ __forceinline__ uint32_t next()
+    __device__ __forceinline__ void init(uint32_t* p_base, uint32_t p, uint32_t s)
     {
-        const uint32_t y = base[pos];
+        base = p_base;
+        pos = p;
+        stale = s;
+        sp = 0;
+        sn = 0;
+        s0 = s1 = s2 = s3 = 0;
+        stg = nullptr;
+    }
+
+    __device__ __forceinline__ void advance()
+    {
         pos++;
         if (pos == MT_N || pos == MT_WORDS) {
             const uint32_t from = pos - MT_N;           // start of the block just finished
@@ -105,7 +142,38 @@ struct MtLane {
             if (stale) mt_twist_serial(base + from, base + pos);   // entering a block nobody refilled yet
             stale = 1;
         }
+    }
+
+    __device__ __forceinline__ uint32_t next()
+    {
+        const uint32_t y = base[pos];
+        advance();
         return mt_temper(y);
+    }
+
+    __device__ __forceinline__ uint32_t staged_offset() const { return pos >= sp ? pos - sp : pos + MT_WORDS - sp; }
+
+    // low 8 bits of the next tempered word
+    __device__ __forceinline__ uint32_t next8()
+    {
+        uint32_t v;
+        if constexpr (MODE == STAGE_NONE) {
+            v = mt_temper(base[pos]) & 255u;
+        } else {
+            const uint32_t k = staged_offset();
+            if (k < sn) {
+                if constexpr (MODE == STAGE_REGS) {
+                    const uint32_t w = k < 8 ? (k < 4 ? s0 : s1) : (k < 12 ? s2 : s3);
+                    v = (w >> (8 * (k & 3))) & 255u;
+                } else {
+                    v = stg[k];
+                }
+            } else {
+                v = mt_temper(base[pos]) & 255u;
+            }
+        }
+        advance();
+        return v;
     }
 
     // numpy random_interval(max): smallest all-ones mask >= max, reject while (u32 & mask) > max
@@ -119,33 +187,131 @@ struct MtLane {
         mask |= mask >> 8;
         mask |= mask >> 16;
         uint32_t v;
-        do {
-            v = next() & mask;
-        } while (v > max);
+        if (max <= 255u) {
+            do {
+                v = next8() & mask;
+            } while (v > max);
+        } else {
+            do {
+                v = next() & mask;
+            } while (v > max);
+        }
         return v;
     }
+
+    // STAGE_REGS restage (per lane, no cross-lane work): a lane with fewer than R staged draws left loads the
+    // 16-word chunk starting at pos & ~3 (four 16-B loads, wrapping at the end of the 1248-word ring), tempers it and
+    // keeps the low bytes. All needy lanes load in the same wave instructions.
+    template <int R>
+    __device__ __forceinline__ void restage_regs()
+    {
+        const uint32_t k = staged_offset();
+        if (k >= sn || sn - k < (uint32_t)R) {
+            const uint32_t a = pos & ~3u;
+            uint32_t w[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                uint32_t q = a + 4u * c;
+                if (q >= (uint32_t)MT_WORDS) q -= MT_WORDS;
+                const uint4 x = *(const uint4*)(base + q);
+                w[c] = (mt_temper(x.x) & 255u) | (mt_temper(x.y) & 255u) << 8 | (mt_temper(x.z) & 255u) << 16 |
+                       (mt_temper(x.w) & 255u) << 24;
+            }
+            s0 = w[0]; s1 = w[1]; s2 = w[2]; s3 = w[3];
+            sp = a;
+            sn = 16;
+        }
+    }
 };
+using MtLane = MtLaneT<STAGE_NONE>;
 
 // End-of-step convergence point: the wave refills every stale block of its lanes. All 64 lanes must call this.
-__device__ __forceinline__ void mt_refill_wave(MtLane& m, int lane)
+template <class M>
+__device__ __forceinline__ void mt_refill_wave(M& m, int lane)
 {
     uint64_t need = __ballot(m.stale != 0);
     while (need) {
         const int j = __builtin_ctzll(need);
         need &= need - 1;
-        const uint64_t b = (uint64_t)(uintptr_t)m.base;
-        // readlane returns int: go through uint32_t so bit 31 of the low half is not sign-extended into the high half
-        const uint64_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, j);
-        const uint64_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), j);
-        const uint32_t* jb = (const uint32_t*)(uintptr_t)(lo | (hi << 32));
+        uint32_t* jb = lane_ptr(m.base, j);
         const uint32_t jpos = __builtin_amdgcn_readlane(m.pos, j);
         const uint32_t cur = jpos < MT_N ? 0 : MT_N;
-        mt_twist_wave(jb + cur, (uint32_t*)jb + (MT_N - cur), lane);
+        mt_twist_wave(jb + cur, jb + (MT_N - cur), lane);
     }
     m.stale = 0;
     // the refilled words are read later by their owner lane of this same wave: order the stores before those loads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// STAGE_LDS rows: W bytes per lane (W multiple of 64), row stride W + 16 (16-B aligned rows for the b128 copies that
+// persist them in HBM between launches; consecutive rows land on shifted banks).
+template <int W>
+struct Stage {
+    static_assert(W % WAVE == 0, "LDS staging rows are filled 64 words per wave instruction");
+    static constexpr int STRIDE = W + 16;
+    static constexpr int BYTES = WAVE * STRIDE;
+};
+
+__device__ __forceinline__ void wave_sync_lds()
+{
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// STAGE_LDS restage, after mt_refill_wave: every lane with fewer than R staged draws left gets its next W words,
+// loaded COALESCED by the whole wave (all 64 lanes read one lane's consecutive words), tempered and packed to bytes
+// (lanes 4q gather lanes 4q+1..3 with DPP row shifts: VALU, no LDS traffic). area = the wave's staging area (lane j's
+// row at area + j * STRIDE). All 64 lanes must call.
+template <int W, int R>
+__device__ __forceinline__ void mt_restage_wave(MtLaneT<STAGE_LDS>& m, uint8_t* area, int lane)
+{
+    constexpr int STRIDE = Stage<W>::STRIDE;
+    m.stg = area + lane * STRIDE;
+    const uint32_t k = m.staged_offset();
+    uint64_t todo = __ballot(k >= m.sn || m.sn - k < (uint32_t)R);
+    while (todo) {
+        const int j = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        const uint32_t* jb = lane_ptr(m.base, j);
+        const uint32_t p = __builtin_amdgcn_readlane(m.pos, j);
+#pragma unroll
+        for (int c = 0; c < W / WAVE; c++) {
+            uint32_t idx = p + (uint32_t)(c * WAVE + lane);
+            if (idx >= (uint32_t)MT_WORDS) idx -= MT_WORDS;
+            const int t = (int)(mt_temper(jb[idx]) & 255u);
+            const uint32_t t1 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x101, 0xF, 0xF, true);  // row_shl:1
+            const uint32_t t2 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x102, 0xF, 0xF, true);  // row_shl:2
+            const uint32_t t3 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x103, 0xF, 0xF, true);  // row_shl:3
+            if ((lane & 3) == 0)
+                *(uint32_t*)(area + j * STRIDE + c * WAVE + lane) = (uint32_t)t | (t1 << 8) | (t2 << 16) | (t3 << 24);
+        }
+        if (lane == j) {
+            m.sp = p;
+            m.sn = W;
+        }
+    }
+    wave_sync_lds();
+}
+
+// Persist / restore a wave's staging rows (W bytes per env, HBM row-major [env][W]) with coalesced 16-B copies, so a
+// launch does not restage every lane from scratch. nvalid = envs of this wave.
+template <int W>
+__device__ __forceinline__ void stage_rows_copy(uint8_t* area, uint8_t* hbm_rows, int lane, int nvalid, bool to_lds)
+{
+    constexpr int STRIDE = Stage<W>::STRIDE, CPR = W / 16;   // 16-B chunks per row
+#pragma unroll
+    for (int i = 0; i < CPR; i++) {
+        const int q = i * WAVE + lane, row = q / CPR, col = q - row * CPR;
+        if (row < nvalid) {
+            uint4* l = (uint4*)(area + row * STRIDE + col * 16);
+            uint4* g = (uint4*)(hbm_rows + (size_t)q * 16);
+            if (to_lds) *l = *g;
+            else *g = *l;
+        }
+    }
+    wave_sync_lds();
 }
 
 // ---- Philox4x32-10 policy RNG: counter (env, t), key = policy seed. Identical to oracle/or_rng.c. ---------------
@@ -187,32 +353,41 @@ template <int ROW>
 struct RowWriter {
     static_assert(ROW % 4 == 0, "byte rows must be dword multiples");
     static constexpr int DW = ROW / 4;
-    static constexpr int STRIDE = DW | 1;
-    static constexpr int LDS_WORDS = WAVE * STRIDE;
+    static constexpr int LDS_WORDS = WAVE * DW;   // the LDS image IS the output span (row-major, no padding)
     static constexpr int NB = (ROW + 31) / 32;
+    static constexpr int Q = (WAVE * DW) / 4;     // 16-B pieces in a full span
 
     __device__ static __forceinline__ uint32_t expand4(uint32_t x)
     {
         return (x & 1u) | ((x & 2u) << 7) | ((x & 4u) << 14) | ((x & 8u) << 21);
     }
 
-    // bits: NB words of a one-bit-per-byte bitmap; out_span: first byte of the wave's 64 rows; nvalid rows written
+    // bits: NB words of a one-bit-per-byte bitmap; out_span: first byte of the wave's 64 rows; nvalid rows written.
+    // LDS writes use an odd stride when DW is odd (conflict-free) and 2-way at worst otherwise; the span leaves LDS
+    // with ds_read_b128 and goes out with 16-B stores (dword stores if the span is not 16-B aligned or partial).
     __device__ static __forceinline__ void write(uint32_t* lds, const uint32_t (&bits)[NB], uint8_t* out_span,
-                                                 int lane, int nvalid)
+                                                 int lane, int nvalid, bool wide = true)
     {
 #pragma unroll
-        for (int j = 0; j < DW; j++) lds[lane * STRIDE + j] = expand4(bits[j / 8] >> (4 * (j % 8)));
+        for (int j = 0; j < DW; j++) lds[lane * DW + j] = expand4(bits[j / 8] >> (4 * (j % 8)));
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        uint32_t* o = (uint32_t*)out_span;
-        const int total = nvalid * DW;
+        if (wide && nvalid == WAVE && (((uintptr_t)out_span) & 15u) == 0) {
+            uint4* o = (uint4*)out_span;
+            const uint4* src = (const uint4*)lds;
 #pragma unroll
-        for (int j = 0; j < DW; j++) {
-            const int e = j * WAVE + lane;
-            if (e < total) {
-                const int r = e / DW, c = e - r * DW;
-                o[e] = lds[r * STRIDE + c];
+            for (int j = 0; j < (Q + WAVE - 1) / WAVE; j++) {
+                const int q = j * WAVE + lane;
+                if (q < Q) o[q] = src[q];
+            }
+        } else {
+            uint32_t* o = (uint32_t*)out_span;
+            const int total = nvalid * DW;
+#pragma unroll
+            for (int j = 0; j < DW; j++) {
+                const int e = j * WAVE + lane;
+                if (e < total) o[e] = lds[e];
             }
         }
         __builtin_amdgcn_wave_barrier();

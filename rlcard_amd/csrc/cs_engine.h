@@ -14,12 +14,15 @@ struct Buffers {
     uint32_t* mt;     // [n][1248]
     uint32_t* ctl;    // [n]
     uint32_t* state;  // [state_words][n]
+    uint32_t* sctl;   // [n] rollout MT staging: staged stream position | staged count << 16
+    uint8_t* sbuf;    // [n][stage bytes] rollout MT staging rows persisted between launches
     const void* table;  // game-specific read-only table (doudizhu action table), or null
     int32_t num_players, num_decks;
     int32_t serial_refill;  // testing hook
 };
 
 int game_info(int32_t game, const cs_config* cfg, cs_game_info* info);
+int64_t stage_bytes_per_env(int32_t game, int32_t num_players);
 
 hipError_t launch_seed(const Buffers& b, const uint32_t* keys_dev, const int32_t* klen_dev, int64_t first,
                        int64_t count, hipStream_t s);

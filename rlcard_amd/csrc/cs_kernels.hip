@@ -64,30 +64,28 @@ __device__ __forceinline__ LaneCtx lane_ctx(int64_t n)
     return c;
 }
 
-__device__ __forceinline__ MtLane mt_lane(uint32_t* mt, const uint32_t* ctl, const LaneCtx& c)
+template <int MODE = STAGE_NONE>
+__device__ __forceinline__ MtLaneT<MODE> mt_lane(uint32_t* mt, const uint32_t* ctl, const LaneCtx& c)
 {
-    MtLane m;
+    MtLaneT<MODE> m;
     if (c.valid) {
         const uint32_t w = ctl[c.env];
-        m.base = mt + c.env * MT_WORDS;
-        m.pos = w & 0x7ffu;
-        m.stale = (w >> 16) & 1u;
+        m.init(mt + c.env * MT_WORDS, w & 0x7ffu, (w >> 16) & 1u);
     } else {
-        m.base = mt;
-        m.pos = 0;
-        m.stale = 0;
+        m.init(mt, 0, 0);
     }
     return m;
 }
 
-__device__ __forceinline__ void refill(MtLane& m, int lane, int serial_only)
+template <class M>
+__device__ __forceinline__ void refill(M& m, int lane, int flags)
 {
-    if (!serial_only) mt_refill_wave(m, lane);
+    if (!(flags & 1)) mt_refill_wave(m, lane);
 }
 
 // obs rows: staged + coalesced when the row is a dword multiple, per-lane bytes otherwise
 template <class G>
-__device__ __forceinline__ void emit_obs(uint32_t* lds, const uint32_t (&bits)[G::NB], uint8_t* obs, int64_t row0,
+__device__ __forceinline__ void emit_obs(uint32_t* lds, const uint32_t (&bits)[G::NB], uint8_t* obs, int64_t row0, int flags,
                                          const LaneCtx& c)
 {
     if constexpr (G::RAW_OBS) {
@@ -97,7 +95,7 @@ __device__ __forceinline__ void emit_obs(uint32_t* lds, const uint32_t (&bits)[G
             for (int k = 0; k < G::OBS; k++) o[k] = (uint8_t)(bits[k >> 2] >> (8 * (k & 3)));
         }
     } else if constexpr (G::OBS % 4 == 0) {
-        RowWriter<G::OBS>::write(lds, bits, obs + row0 * G::OBS, c.lane, c.nvalid);
+        RowWriter<G::OBS>::write(lds, bits, obs + row0 * G::OBS, c.lane, c.nvalid, !(flags & 4));
     } else {
         if (c.valid) {
             uint8_t* o = obs + (row0 + c.lane) * G::OBS;
@@ -137,6 +135,25 @@ template <class G>
 struct ObsLds {
     static constexpr int WORDS = ObsWords<G::OBS, !G::RAW_OBS && G::OBS % 4 == 0>::value;
 };
+template <int W, bool LDS>
+struct StageBytesOf {
+    static constexpr int value = 16;
+};
+template <int W>
+struct StageBytesOf<W, true> {
+    static constexpr int value = Stage<W>::BYTES;
+};
+template <class G>
+struct StageBytes {
+    static constexpr int value = StageBytesOf<G::STAGE_W, G::STAGE_MODE == STAGE_LDS>::value;
+};
+// restage after the refill, per the game's staging mode (see MtLaneT)
+template <class G, class M>
+__device__ __forceinline__ void restage(M& m, uint8_t* area, int lane)
+{
+    if constexpr (G::STAGE_MODE == STAGE_REGS) m.template restage_regs<G::STAGE_R>();
+    else if constexpr (G::STAGE_MODE == STAGE_LDS) mt_restage_wave<G::STAGE_W, G::STAGE_R>(m, area, lane);
+}
 template <class G>
 struct Scratch {
     static constexpr int WORDS = (G::SCRATCH_WORDS > 0 ? G::SCRATCH_WORDS : 1) * WAVE;
@@ -149,7 +166,7 @@ struct Scratch {
 template <class G>
 __global__ __launch_bounds__(BLOCK) void k_seed(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
                                                  const uint32_t* keys, const int32_t* klen, int64_t first,
-                                                 int64_t count, int serial_only, GameParams prm)
+                                                 int64_t count, int flags, GameParams prm)
 {
     __shared__ uint32_t scr[WAVES_PER_BLOCK][Scratch<G>::WORDS];
     const int lane = threadIdx.x & (WAVE - 1);
@@ -157,9 +174,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed(uint32_t* mt, uint32_t* ctl, uin
     const bool valid = i < count;
     const int64_t env = first + i;
     MtLane m;
-    m.base = mt;
-    m.pos = 0;
-    m.stale = 0;
+    m.init(mt, 0, 0);
     if (valid) {
         uint32_t* base = mt + env * MT_WORDS;
         const int kl = klen[i] == 2 ? 2 : 1;                    // validated on the host; never trust it here
@@ -172,7 +187,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed(uint32_t* mt, uint32_t* ctl, uin
         g.blank();
         g.store(st, n, env);
     }
-    if (serial_only) {
+    if (flags & 1) {
         if (valid) mt_twist_serial(m.base, m.base + MT_N);
         m.stale = 0;
     } else {
@@ -183,7 +198,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed(uint32_t* mt, uint32_t* ctl, uin
 
 template <class G>
 __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
-                                                  cs_step_out out, int serial_only, GameParams prm)
+                                                  cs_step_out out, int flags, GameParams prm)
 {
     CS_SMEM(G);
     const LaneCtx c = lane_ctx(n);
@@ -195,11 +210,11 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, ui
         g.load(st, n, c.env);   // the Game object outlives init_game (limit-holdem's raise history, :98/:101)
         g.reset(m);
     }
-    refill(m, c.lane, serial_only);
+    refill(m, c.lane, flags & 1);
     uint32_t bits[G::NB];
     const int p = g.current();
     g.observe(p, bits);
-    if (out.obs) emit_obs<G>(lds[c.wid], bits, (uint8_t*)out.obs, c.wave_first, c);
+    if (out.obs) emit_obs<G>(lds[c.wid], bits, (uint8_t*)out.obs, c.wave_first, flags, c);
     if (c.valid) {
         if (out.legal) emit_legal<G>((uint8_t*)out.legal, c.env, g.legal());
         if (out.player) ((uint8_t*)out.player)[c.env] = (uint8_t)p;
@@ -217,7 +232,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, ui
 
 template <class G>
 __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
-                                                 const int32_t* actions, cs_step_out out, int serial_only,
+                                                 const int32_t* actions, cs_step_out out, int flags,
                                                  GameParams prm)
 {
     CS_SMEM(G);
@@ -240,11 +255,11 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uin
             if (done) g.payoffs(r);
         }
     }
-    refill(m, c.lane, serial_only);
+    refill(m, c.lane, flags & 1);
     uint32_t bits[G::NB];
     const int p = g.current();
     g.observe(p, bits);
-    if (out.obs) emit_obs<G>(lds[c.wid], bits, (uint8_t*)out.obs, c.wave_first, c);
+    if (out.obs) emit_obs<G>(lds[c.wid], bits, (uint8_t*)out.obs, c.wave_first, flags, c);
     if (c.valid) {
         if (out.legal) emit_legal<G>((uint8_t*)out.legal, c.env, g.legal());
         if (out.player) ((uint8_t*)out.player)[c.env] = (uint8_t)p;
@@ -267,7 +282,7 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n
     if (c.valid) g.load(st, n, c.env);
     uint32_t bits[G::NB];
     g.observe(player, bits);
-    if (out.obs) emit_obs<G>(lds[c.wid], bits, (uint8_t*)out.obs, c.wave_first, c);
+    if (out.obs) emit_obs<G>(lds[c.wid], bits, (uint8_t*)out.obs, c.wave_first, 0, c);
     if (c.valid) {
         if (out.legal) emit_legal<G>((uint8_t*)out.legal, c.env, g.legal());
         if (out.player) ((uint8_t*)out.player)[c.env] = (uint8_t)g.current();
@@ -278,11 +293,30 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n
 template <class G>
 __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n, int T,
                                                     uint64_t seed, uint64_t t0, uint64_t env_base, cs_traj_out out,
-                                                    int serial_only, GameParams prm)
+                                                    int flags, GameParams prm, uint32_t* sctl, uint8_t* sbuf)
 {
     CS_SMEM(G);
+    __shared__ __attribute__((aligned(16))) uint8_t stage[WAVES_PER_BLOCK][StageBytes<G>::value];
     const LaneCtx c = lane_ctx(n);
-    MtLane m = mt_lane(mt, ctl, c);
+    MtLaneT<G::STAGE_MODE> m = mt_lane<G::STAGE_MODE>(mt, ctl, c);
+    // MT staging needs both blocks valid at every restage, i.e. the cooperative refill (flag bit 0 off);
+    // flag bit 1 disables it (one global load per draw) for A/B runs and fallback-path tests
+    const bool staged = !(flags & 3);
+    constexpr bool persist = G::STAGE_MODE == STAGE_LDS;
+    uint8_t* rows = nullptr;
+    if constexpr (persist) {
+        // the staged rows left by the previous launch stay valid while ctl bit 17 is set (single-step kernels and
+        // seeding rewrite ctl without it)
+        rows = sbuf + c.wave_first * G::STAGE_W;
+        if (staged) {
+            if (c.valid && ((ctl[c.env] >> 17) & 1u)) {
+                const uint32_t w = sctl[c.env];
+                m.sp = w & 0xFFFFu;
+                m.sn = w >> 16;
+            }
+            stage_rows_copy<G::STAGE_W>(stage[c.wid], rows, c.lane, c.nvalid, true);
+        }
+    }
     G g;
     g.bind(&scr[c.wid][c.lane], prm);
     g.blank();
@@ -290,7 +324,8 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, 
         g.load(st, n, c.env);
         if (g.is_over()) g.reset(m);
     }
-    refill(m, c.lane, serial_only);
+    refill(m, c.lane, flags & 1);
+    if (staged) restage<G>(m, stage[c.wid], c.lane);
     uint8_t* obs = (uint8_t*)out.obs;
     uint8_t* legal = (uint8_t*)out.legal;
     uint8_t* player = (uint8_t*)out.player;
@@ -298,13 +333,14 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, 
     uint8_t* done_o = (uint8_t*)out.done;
     const uint64_t genv = env_base + (uint64_t)c.env;
     for (int t = 0; t < T; t++) {
+
         const int64_t rowbase = (int64_t)t * n;
         const int p = g.current();
         const uint64_t lg = g.legal();
         uint32_t bits[G::NB];
         g.observe(p, bits);
         const int a = pick_legal(lg, philox_u32(seed, genv, t0 + (uint64_t)t));
-        emit_obs<G>(lds[c.wid], bits, obs, rowbase + c.wave_first, c);
+        emit_obs<G>(lds[c.wid], bits, obs, rowbase + c.wave_first, flags, c);
         float r[G::P];
 #pragma unroll
         for (int k = 0; k < G::P; k++) r[k] = 0.f;
@@ -322,11 +358,20 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, 
             done_o[row] = (uint8_t)done;
             if (done) g.reset(m);
         }
-        refill(m, c.lane, serial_only);
+        refill(m, c.lane, flags & 1);
+        if (staged) restage<G>(m, stage[c.wid], c.lane);
+    }
+    bool keep = false;
+    if constexpr (persist) {
+        if (staged) {
+            stage_rows_copy<G::STAGE_W>(stage[c.wid], rows, c.lane, c.nvalid, false);
+            keep = true;
+        }
     }
     if (c.valid) {
         g.store(st, n, c.env);
-        ctl[c.env] = m.pos | (m.stale << 16);
+        ctl[c.env] = m.pos | (m.stale << 16) | ((uint32_t)keep << 17);
+        if (keep) sctl[c.env] = m.sp | (m.sn << 16);
     }
 }
 
@@ -366,7 +411,7 @@ static hipError_t rollout_g(const Buffers& b, int32_t T, uint64_t seed, uint64_t
                             const cs_traj_out& o, hipStream_t s)
 {
     hipLaunchKernelGGL(k_rollout<G>, grid_for(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0,
-                       env_base, o, b.serial_refill, params_of(b));
+                       env_base, o, b.serial_refill, params_of(b), b.sctl, b.sbuf);
     return hipGetLastError();
 }
 
@@ -379,6 +424,19 @@ static void fill_info(cs_game_info* info)
     info->legal_bytes = G::LB;
     info->action_bytes = G::ACTION_BYTES;
     info->state_words = G::WORDS;
+}
+
+template <class G>
+static int64_t stage_bytes_of() { return G::STAGE_MODE == STAGE_LDS ? G::STAGE_W : 0; }
+
+int64_t stage_bytes_per_env(int32_t game, int32_t num_players)
+{
+    switch (game) {
+    case CS_GAME_LEDUC: return stage_bytes_of<Leduc>();
+    case CS_GAME_LIMIT: return stage_bytes_of<Limit>();
+    case CS_GAME_BLACKJACK: return num_players <= 1 ? stage_bytes_of<Blackjack<1>>() : stage_bytes_of<Blackjack<4>>();
+    default: return 0;
+    }
 }
 
 int game_info(int32_t game, const cs_config* cfg, cs_game_info* info)

@@ -15,6 +15,11 @@
 #pragma once
 #include "cs_device.h"
 
+#ifndef CS_LEDUC_STAGE_R
+
+#define CS_LEDUC_STAGE_R 12
+#endif
+
 namespace cs {
 
 struct Leduc {
@@ -22,6 +27,7 @@ struct Leduc {
     static constexpr int NB = 2;  // obs bitmap words
     static constexpr bool RAW_OBS = false;
     static constexpr int SCRATCH_WORDS = 0;
+    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 64, STAGE_R = CS_LEDUC_STAGE_R;  // MT staging (see MtLaneT)
     __device__ __forceinline__ void bind(uint32_t*, const GameParams&) {}
     enum { CALL = 0, RAISE = 1, FOLD = 2, CHECK = 3 };
 
@@ -66,7 +72,8 @@ struct Leduc {
         set_bit(bits, in0 + in1 - my + 21);
     }
 
-    __device__ __forceinline__ void reset(MtLane& rng)
+    template <class Rng>
+    __device__ __forceinline__ void reset(Rng& rng)
     {
         uint32_t deck = 0x543210u;  // nibble i = card at deck position i
 #pragma unroll
@@ -84,7 +91,8 @@ struct Leduc {
         hr = 0; nrn = 0; rc = 0; f0 = 0; f1 = 0; over = 0;
     }
 
-    __device__ __forceinline__ void step(int a, MtLane&)
+    template <class Rng>
+    __device__ __forceinline__ void step(int a, Rng&)
     {
         const uint32_t lg = legal();
         if (a < 0 || a > 3 || !((lg >> a) & 1u)) a = ((lg >> CHECK) & 1u) ? CHECK : FOLD;

@@ -101,6 +101,7 @@ struct Limit {
     static constexpr int NB = 3;
     static constexpr bool RAW_OBS = false;
     static constexpr int SCRATCH_WORDS = 0;
+    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_R = 100;  // MT staging (see MtLaneT)
     __device__ __forceinline__ void bind(uint32_t*, const GameParams&) {}
     enum { CALL = 0, RAISE = 1, FOLD = 2, CHECK = 3 };
 
@@ -158,7 +159,8 @@ struct Limit {
         for (int i = 0; i < 4; i++) set_bit(bits, 52 + 5 * i + (int)((rn >> (3 * i)) & 7u));
     }
 
-    __device__ __forceinline__ void reset(MtLane& rng)
+    template <class Rng>
+    __device__ __forceinline__ void reset(Rng& rng)
     {
         int J[9], V[9], D[9];
 #pragma unroll
@@ -188,7 +190,8 @@ struct Limit {
         w3 = (w3 & 0xFFFu) << 12;                                                      // prev <- current, current <- 0
     }
 
-    __device__ __forceinline__ void step(int a, MtLane&)
+    template <class Rng>
+    __device__ __forceinline__ void step(int a, Rng&)
     {
         const uint32_t lg = legal();
         if (a < 0 || a > 3 || !((lg >> a) & 1u)) a = ((lg >> CHECK) & 1u) ? CHECK : FOLD;

@@ -158,5 +158,8 @@ class VecEnv:
         _abi.check(_abi.lib().cs_get_rng_ctl(self._h, int(env), C.byref(v)), 'cs_get_rng_ctl')
         return v.value & 0x7FF
 
+    def set_kernel_flags(self, flags):
+        _abi.check(_abi.lib().cs_debug_set_kernel_flags(self._h, int(flags)), 'cs_debug_set_kernel_flags')
+
     def set_serial_refill(self, enable):
         _abi.check(_abi.lib().cs_debug_set_serial_refill(self._h, 1 if enable else 0), 'cs_debug_set_serial_refill')

@@ -112,13 +112,13 @@ def test_step_api_matches_oracle(oracle, game, name):
             assert np.array_equal(o['obs'][i], obs) and np.array_equal(o['legal'][i], legal)
 
 
-@pytest.mark.parametrize('serial', [False, True])
+@pytest.mark.parametrize('flags', [0, 1, 2, 4, 7])   # kernel variants: serial refill / per-draw loads / dword stores
 @pytest.mark.parametrize('game,name', GAMES)
-def test_rollout_matches_oracle(oracle, game, name, serial):
+def test_rollout_matches_oracle(oracle, game, name, flags):
     n, T = 4160 + 37, 48
     seeds = list(range(7, 7 + n))
     v = _vec(game, n, seed=7)
-    v.set_serial_refill(serial)
+    v.set_kernel_flags(flags)
     ob = _oracle_batch(oracle, game, seeds)
     v.reset()
     ob.reset()

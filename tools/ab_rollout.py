@@ -1,0 +1,35 @@
+"""A/B timing of k_rollout kernel variants (cs_debug_set_kernel_flags) interleaved in ONE process (rule 24).
+  python tools/ab_rollout.py GAME N T flagsA flagsB ..."""
+import sys
+import statistics
+
+import torch
+
+sys.path.insert(0, '.')
+from rlcard_amd import VecEnv  # noqa: E402
+
+game, n, T = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+variants = [int(x) for x in sys.argv[4:]] or [0, 2, 4, 6]
+v = VecEnv(game, n, seed=42, device=0)
+v.reset()
+tr = v.new_traj_out(T)
+t = 0
+for f in variants:            # warm-up each variant
+    v.set_kernel_flags(f)
+    v.rollout(T, 5, t * T, out=tr); t += 1
+torch.cuda.synchronize()
+times = {f: [] for f in variants}
+for rnd in range(6):
+    for f in variants:
+        v.set_kernel_flags(f)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for k in range(5):
+            v.rollout(T, 5, t * T, out=tr); t += 1
+        e1.record()
+        torch.cuda.synchronize()
+        times[f].append(e0.elapsed_time(e1) / 5)
+for f in variants:
+    med = statistics.median(times[f])
+    print('%s n=%d T=%d flags=%d: median %.3f ms/launch (min %.3f) -> %.3g env-steps/s' % (
+        game, n, T, f, med, min(times[f]), n * T / (med * 1e-3)), flush=True)
