@@ -117,10 +117,35 @@ static void legal_bits(const ddz_env *e, uint8_t *bits)
     }
 }
 
+/* One id against the rules of legal_bits (no table scan). */
+static int is_legal(const ddz_env *e, int a)
+{
+    if (a < 0 || a >= NA) return 0;
+    const int leading = e->greater < 0 || e->greater == e->current;
+    if (a == PASS) return !leading;
+    if (!contains(e->hand[e->current], a)) return 0;
+    if (leading) return 1;
+    const int tt = T_type[e->greater_play], tw = T_weight[e->greater_play], ty = T_type[a];
+    if (tt == T_rocket) return 0;
+    return (ty == tt && T_weight[a] > tw) || ty == T_rocket || (ty == T_bomb && tt != T_bomb);
+}
+
+/* The reference applies any id (an illegal one corrupts the hands, player.py:88-108); the engine's ABI replaces an
+ * id outside the legal set by the lowest solo when leading and by pass when following (include/cardsim.h cs_step). */
+static int decode(const ddz_env *e, int a)
+{
+    if (is_legal(e, a)) return a;
+    if (!(e->greater < 0 || e->greater == e->current)) return PASS;
+    for (int r = 0; r < 15; r++)
+        if (e->hand[e->current][r]) return r;          /* solo ids 0..14 = ranks (tests/golden/ddz_actions.npz) */
+    return PASS;
+}
+
 static void d_step(void *v, or_mt *rng, int a)
 {
     (void)rng;
     ddz_env *e = (ddz_env *)v;
+    a = decode(e, a);
     const int p = e->current;
     if (e->ntrace < MAXTRACE) {
         e->trace_p[e->ntrace] = (int16_t)p;

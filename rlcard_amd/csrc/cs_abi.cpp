@@ -6,12 +6,21 @@
 #include <new>
 #include <string>
 #include "cs_engine.h"
+#include "cs_doudizhu.h"
+
+namespace cs {
+namespace ddz {
+std::string table_create(void** dev, Tab* tab);
+}
+}  // namespace cs
 
 struct cs_handle {
     cs::Buffers b;
     cs_game_info info;
     int32_t device;
     bool seeded;
+    void* table_dev;     // doudizhu: device action table (one allocation)
+    cs::ddz::Tab tab;    // doudizhu: views into it, passed to the kernels by value
 };
 
 namespace {
@@ -81,6 +90,14 @@ int cs_create(cs_handle** out, int32_t game, int64_t num_envs, int32_t device, c
         cs_destroy(h);
         return fail_hip(e, "hipMalloc (env state)");
     }
+    if (game == CS_GAME_DOUDIZHU) {
+        const std::string err = cs::ddz::table_create(&h->table_dev, &h->tab);
+        if (!err.empty()) {
+            cs_destroy(h);
+            return fail(CS_E_DEVICE, err.c_str());
+        }
+        h->b.table = &h->tab;
+    }
     const int64_t sb = cs::stage_bytes_per_env(game, info.num_players);
     if (sb > 0) {   // rollout staging rows, whole waves (the copy moves 16-B chunks of full rows)
         const size_t rows = (n + 63) / 64 * 64;
@@ -103,6 +120,7 @@ void cs_destroy(cs_handle* h)
     if (h->b.state) (void)hipFree(h->b.state);
     if (h->b.sctl) (void)hipFree(h->b.sctl);
     if (h->b.sbuf) (void)hipFree(h->b.sbuf);
+    if (h->table_dev) (void)hipFree(h->table_dev);
     delete h;
 }
 
@@ -188,8 +206,15 @@ int cs_get_env_state(cs_handle* h, int64_t env, uint32_t* host_words, int32_t nw
     int r = set_device(h);
     if (r != CS_OK) return r;
     hipError_t e = hipDeviceSynchronize();
-    for (int w = 0; w < h->info.state_words && e == hipSuccess; w++)
-        e = hipMemcpy(host_words + w, h->b.state + (size_t)w * h->b.n + env, sizeof(uint32_t), hipMemcpyDeviceToHost);
+    const int sw = h->info.state_words;
+    if (cs::state_env_major(h->b.game)) {
+        if (e == hipSuccess)
+            e = hipMemcpy(host_words, h->b.state + (size_t)env * sw, sizeof(uint32_t) * sw, hipMemcpyDeviceToHost);
+    } else {
+        for (int w = 0; w < sw && e == hipSuccess; w++)
+            e = hipMemcpy(host_words + w, h->b.state + (size_t)w * h->b.n + env, sizeof(uint32_t),
+                          hipMemcpyDeviceToHost);
+    }
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_get_env_state");
 }
 

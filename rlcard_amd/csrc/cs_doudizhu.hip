@@ -1,0 +1,710 @@
+// cs_doudizhu.hip -- DouDizhu lockstep kernels for gfx950: ONE WAVE PER ENV.
+//
+// Per step a wave
+//   1. builds the 27 472-bit legal mask in LDS (Judger.playable_cards_from_hand / get_gt_cards,
+//      rlcard/games/doudizhu/judger.py:124-331, utils.py:517-621): the legal set of a hand is every table combo the
+//      hand contains (leading), or pass + same-type greater-weight combos + bombs + rocket (following). Three passes,
+//      all 64 lanes wide:
+//        a. the 308 (type, weight) groups: does the hand contain the group's elementwise-min combo (and may the group
+//           be played now)? -> ballot + prefix counts in LDS;
+//        b. the 859 mask dwords: does any of the groups overlapping the dword pass? (two LDS reads per dword);
+//        c. the few dwords that survive (about 6 for a 17-card hand): 32 lanes test one id each against the hand
+//           (SWAR containment on packed nibble counts), ballot = the mask dword.
+//   2. builds the obs row (envs/doudizhu.py:26-134) as a bit vector in LDS: 54-bit card blocks (_cards2array is a
+//      thermometer code of every rank nibble, computed with four SWAR adds), the one-hot hand sizes;
+//   3. writes both rows with 16-B stores at whatever alignment the row has (boundary chunks byte by byte);
+//   4. (rollout) picks the policy action: uniform over the legal ids from Philox(seed, env, t) -- the k-th set bit
+//      found with a wave prefix scan over the surviving dwords;
+//   5. applies the action with wave-uniform (scalar) updates of the packed state (round.py:67-79, game.py:55-81).
+// The deal (dealer.py:12-76: one 54-card np.random shuffle) runs the Fisher-Yates loop with the deck held one card
+// per lane and the MT19937 words loaded 64 at a time (coalesced) and consumed with readlane.
+// Output bytes per env-step: 901 obs + 3 434 legal + 12 reward + 4 -- HBM-bound by design.
+#include "cs_device.h"
+#include "cs_engine.h"
+#include "cs_doudizhu.h"
+
+namespace cs {
+namespace ddz {
+
+constexpr int BLOCK = 256;
+constexpr int WPB = BLOCK / WAVE;
+constexpr int MASK_PAD = 4;                       // zero dwords on both sides of the mask image
+constexpr int MASK_WORDS = MASK_PAD + 860 + MASK_PAD;
+constexpr int NSEG = 20;                          // 54-bit obs blocks (16 used) + zero tail
+constexpr int BV_WORDS = 32;                      // obs bits (912 + 16 front pad) as dwords
+
+struct WaveLds {
+    uint32_t mask[MASK_WORDS];   // legal bits: id i at bit (i & 31) of mask[MASK_PAD + i / 32]
+    uint64_t segv[NSEG];         // obs 54-bit blocks
+    uint32_t bv[BV_WORDS];       // obs bit x at bit 16 + x
+    uint16_t pre[MAX_GROUPS + 8];
+    uint16_t list[ND + 1];       // mask dwords that survived pass b, ascending
+};
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, k); }
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int k)
+{
+    return (uint64_t)rl((uint32_t)v, k) | ((uint64_t)rl((uint32_t)(v >> 32), k) << 32);
+}
+__device__ __forceinline__ uint32_t mbcnt(uint64_t b)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+}
+__device__ __forceinline__ bool contains(uint64_t hand, uint64_t combo)
+{
+    return (((hand | NIB_HI) - combo) & NIB_HI) == NIB_HI;
+}
+// _cards2array (envs/doudizhu.py:150-166) of packed counts: bit 4r + k = (count_r > k) for r < 13, bit 52 / 53 = jokers
+__device__ __forceinline__ uint64_t cards_bits(uint64_t c)
+{
+    const uint64_t lo = c & 0x000FFFFFFFFFFFFFull, H = 0x0008888888888888ull;
+    const uint64_t t = (((lo + 0x0007777777777777ull) & H) >> 3) | (((lo + 0x0006666666666666ull) & H) >> 2) |
+                       (((lo + 0x0005555555555555ull) & H) >> 1) | ((lo + 0x0004444444444444ull) & H);
+    return t | ((uint64_t)(((c >> 52) & 15u) != 0) << 52) | ((uint64_t)(((c >> 56) & 15u) != 0) << 53);
+}
+__device__ __forceinline__ uint32_t num_cards(uint64_t c)
+{
+    const uint64_t b = (c & 0x0F0F0F0F0F0F0F0Full) + ((c >> 4) & 0x0F0F0F0F0F0F0F0Full);
+    return (uint32_t)((b * 0x0101010101010101ull) >> 56);
+}
+
+// x if c else 0, written so that a choice between fields of a local struct stays a register operation (a plain
+// `c ? s.a : s.b` is folded into a load from a computed field address, which sends the whole struct to scratch)
+__device__ __forceinline__ uint64_t keep64(bool c, uint64_t x) { return x & (0ull - (uint64_t)c); }
+__device__ __forceinline__ uint32_t keep32(bool c, uint32_t x) { return x & (0u - (uint32_t)c); }
+
+// ---- wave-uniform env state -------------------------------------------------------------------------------------
+struct Env {
+    uint64_t h0, h1, h2;        // hands
+    uint64_t q0, q1, q2;        // played
+    // the last 9 trace ids, oldest first, two per word (id k at bits 16 * (k & 1) of word k / 2; the high half of
+    // hw4 is unused). Separate scalars, not an array: a lane-indexed pick from an array sends it to scratch.
+    uint32_t hw0, hw1, hw2, hw3, hw4;
+    uint32_t ntrace, greater, gplay, cur, winner;
+
+    __device__ __forceinline__ uint32_t hist(uint32_t k) const   // k may differ per lane
+    {
+        const uint32_t j = k >> 1;
+        const uint32_t w = keep32(j == 0, hw0) | keep32(j == 1, hw1) | keep32(j == 2, hw2) | keep32(j == 3, hw3) |
+                           keep32(j == 4, hw4);
+        return (w >> (16 * (k & 1))) & 0xFFFFu;
+    }
+
+    __device__ __forceinline__ uint64_t hand(uint32_t p) const
+    {
+        return keep64(p == 0, h0) | keep64(p == 1, h1) | keep64(p == 2, h2);
+    }
+    __device__ __forceinline__ uint64_t played(uint32_t p) const
+    {
+        return keep64(p == 0, q0) | keep64(p == 1, q1) | keep64(p == 2, q2);
+    }
+    __device__ __forceinline__ bool over() const { return winner != NONE; }
+
+    __device__ __forceinline__ void load(const uint32_t* st, int64_t env, int lane)
+    {
+        const uint32_t w = lane < WORDS ? st[env * WORDS + lane] : 0u;
+        h0 = (uint64_t)rl(w, 0) | ((uint64_t)rl(w, 1) << 32);
+        h1 = (uint64_t)rl(w, 2) | ((uint64_t)rl(w, 3) << 32);
+        h2 = (uint64_t)rl(w, 4) | ((uint64_t)rl(w, 5) << 32);
+        q0 = (uint64_t)rl(w, 6) | ((uint64_t)rl(w, 7) << 32);
+        q1 = (uint64_t)rl(w, 8) | ((uint64_t)rl(w, 9) << 32);
+        q2 = (uint64_t)rl(w, 10) | ((uint64_t)rl(w, 11) << 32);
+        hw0 = rl(w, W_HIST);
+        hw1 = rl(w, W_HIST + 1);
+        hw2 = rl(w, W_HIST + 2);
+        hw3 = rl(w, W_HIST + 3);
+        hw4 = rl(w, W_HIST + 4) | (NO_ACTION << 16);
+        ntrace = rl(w, W_NTRACE);
+        const uint32_t g = rl(w, W_GREATER), c = rl(w, W_CUR);
+        greater = g & 0xFFFFu;
+        gplay = g >> 16;
+        cur = c & 0xFFu;
+        winner = (c >> 8) & 0xFFu;
+    }
+    __device__ __forceinline__ void store(uint32_t* st, int64_t env, int lane) const
+    {
+        if (lane == 0) {
+            uint4* o = (uint4*)(st + env * WORDS);   // 80-B rows: 16-B aligned
+            o[0] = make_uint4((uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32));
+            o[1] = make_uint4((uint32_t)h2, (uint32_t)(h2 >> 32), (uint32_t)q0, (uint32_t)(q0 >> 32));
+            o[2] = make_uint4((uint32_t)q1, (uint32_t)(q1 >> 32), (uint32_t)q2, (uint32_t)(q2 >> 32));
+            o[3] = make_uint4(hw0, hw1, hw2, hw3);
+            o[4] = make_uint4(hw4, ntrace, greater | (gplay << 16), cur | (winner << 8));
+        }
+    }
+
+    // Player.play + Round.proceed_round + Game.step (player.py:88-108, round.py:54-79, game.py:55-81)
+    __device__ __forceinline__ void apply(uint32_t a, const Tab& tb)
+    {
+        const uint32_t p = cur;
+        hw0 = (hw0 >> 16) | (hw1 << 16);
+        hw1 = (hw1 >> 16) | (hw2 << 16);
+        hw2 = (hw2 >> 16) | (hw3 << 16);
+        hw3 = (hw3 >> 16) | (hw4 << 16);
+        hw4 = a | (NO_ACTION << 16);
+        ntrace++;
+        if (a != (uint32_t)PASS) {
+            const uint64_t c = tb.cnt[a];
+            const uint64_t c0 = keep64(p == 0, c), c1 = keep64(p == 1, c), c2 = keep64(p == 2, c);
+            h0 -= c0; h1 -= c1; h2 -= c2;
+            q0 += c0; q1 += c1; q2 += c2;
+            const uint64_t left = hand(p);
+            greater = p;
+            gplay = a;
+            if (left == 0) winner = p;
+        }
+        cur = p == 2 ? 0u : p + 1;
+    }
+};
+
+// the ids a player may play now: leading -> every combo; following -> [c_lo, c_lo + c_len) (same type, greater
+// weight), the bombs unless the last play is a bomb, the rocket; nothing after a rocket (utils.py:590-621)
+struct Cand {
+    uint32_t c_lo, c_len, b_lo, b_len, r_lo, r_len;
+    bool leading;
+    __device__ __forceinline__ bool ok(uint32_t x) const
+    {
+        return (x - c_lo < c_len) | (x - b_lo < b_len) | (x - r_lo < r_len);
+    }
+};
+__device__ __forceinline__ Cand cand_of(const Env& e, const Tab& tb)
+{
+    Cand c;
+    c.leading = e.greater == NONE || e.greater == e.cur;   // player.py:60-86 available_actions
+    if (c.leading) {
+        c.c_lo = 0; c.c_len = PASS; c.b_lo = 0; c.b_len = 0; c.r_lo = 0; c.r_len = 0;
+        return c;
+    }
+    const uint32_t g = tb.gid[e.gplay];
+    const uint32_t z = tb.grp[g * 4 + 2], y = tb.grp[g * 4 + 3];
+    const uint32_t gend = z >> 16, tend = y & 0xFFFFu, type = (y >> 16) & 0xFFu;
+    if (type == (uint32_t)TYPE_ROCKET) {
+        c.c_lo = 0; c.c_len = 0; c.b_lo = 0; c.b_len = 0; c.r_lo = 0; c.r_len = 0;
+        return c;
+    }
+    c.c_lo = gend;
+    c.c_len = tend - gend;
+    c.b_lo = (uint32_t)tb.bomb_lo;
+    c.b_len = type == (uint32_t)TYPE_BOMB ? 0u : (uint32_t)(tb.bomb_hi - tb.bomb_lo);
+    c.r_lo = (uint32_t)tb.rocket;
+    c.r_len = 1;
+    return c;
+}
+
+// single-id legality + the fallback for an id outside the legal set (cs_step only; the reference has no decode
+// fallback for doudizhu -- an illegal id corrupts its hands -- so the ABI defines one: lowest solo when leading,
+// pass when following)
+__device__ __forceinline__ uint32_t decode_action(int32_t a, const Env& e, const Cand& c, const Tab& tb)
+{
+    const uint64_t h = e.hand(e.cur);
+    bool ok;
+    if (a < 0 || a >= NA) ok = false;
+    else if (a == PASS) ok = !c.leading;
+    else ok = contains(h, tb.cnt[a]) && c.ok((uint32_t)a);
+    if (ok) return (uint32_t)a;
+    if (!c.leading) return (uint32_t)PASS;
+    const uint64_t nz = (h | (h >> 1) | (h >> 2)) & 0x0111111111111111ull;
+    return (uint32_t)(__builtin_ctzll(nz) >> 2);   // solo id = rank (checked by the table builder)
+}
+
+// ---- MT19937 stream of this env, read by the whole wave --------------------------------------------------------
+struct WaveMt {
+    uint32_t* base;
+    uint32_t pos, stale;
+    // 64 tempered words from pos (lane k: word pos + k); twists the next block first if the window reaches it
+    __device__ __forceinline__ uint32_t window(int lane)
+    {
+        const uint32_t end = pos < (uint32_t)MT_N ? (uint32_t)MT_N : (uint32_t)MT_WORDS;
+        if (stale && pos + WAVE > end) {
+            const uint32_t cur = pos < (uint32_t)MT_N ? 0u : (uint32_t)MT_N;
+            mt_twist_wave(base + cur, base + (MT_N - cur), lane);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            stale = 0;
+        }
+        uint32_t idx = pos + (uint32_t)lane;
+        if (idx >= (uint32_t)MT_WORDS) idx -= MT_WORDS;
+        return mt_temper(base[idx]);
+    }
+    __device__ __forceinline__ void advance(uint32_t k)
+    {
+        uint32_t np = pos + k;
+        const bool crossed = pos < (uint32_t)MT_N ? np >= (uint32_t)MT_N : np >= (uint32_t)MT_WORDS;
+        if (np >= (uint32_t)MT_WORDS) np -= MT_WORDS;
+        if (crossed) stale = 1;
+        pos = np;
+    }
+};
+
+// Dealer.shuffle + deal_cards + landlord's 3 cards (dealer.py:12-76; game.py:23-53): np.random.shuffle of the
+// sorted 54-card deck (position k holds rank k / 4, 52 = black joker, 53 = red joker), hands deck[0:17] (landlord),
+// [17:34], [34:51], landlord + deck[51:54]
+__device__ __forceinline__ void deal(Env& e, WaveMt& m, int lane)
+{
+    uint32_t deck = (uint32_t)lane;
+    uint32_t win = m.window(lane);
+    uint32_t wi = 0;
+    for (int i = 53; i >= 1; i--) {
+        uint32_t mask = (uint32_t)i;
+        mask |= mask >> 1;
+        mask |= mask >> 2;
+        mask |= mask >> 4;
+        uint32_t u;
+        do {
+            if (wi == (uint32_t)WAVE) {
+                m.advance(WAVE);
+                win = m.window(lane);
+                wi = 0;
+            }
+            u = rl(win, (int)wi) & mask;
+            wi++;
+        } while (u > (uint32_t)i);
+        const uint32_t vi = rl(deck, i), vu = rl(deck, (int)u);
+        deck = lane == i ? vu : (lane == (int)u ? vi : deck);
+    }
+    m.advance(wi);
+    const uint32_t rank = deck < 52u ? deck >> 2 : deck - 39u;
+    const uint64_t own0 = 0x003800000001FFFFull, own1 = 0x00000003FFFE0000ull, own2 = 0x0007FFFC00000000ull;
+    uint64_t h0 = 0, h1 = 0, h2 = 0;
+#pragma unroll
+    for (int r = 0; r < 15; r++) {
+        const uint64_t b = __ballot(lane < 54 && rank == (uint32_t)r);
+        h0 |= (uint64_t)__popcll(b & own0) << (4 * r);
+        h1 |= (uint64_t)__popcll(b & own1) << (4 * r);
+        h2 |= (uint64_t)__popcll(b & own2) << (4 * r);
+    }
+    e.h0 = h0; e.h1 = h1; e.h2 = h2;
+    e.q0 = e.q1 = e.q2 = 0;
+    e.hw0 = e.hw1 = e.hw2 = e.hw3 = e.hw4 = 0xFFFFFFFFu;
+    e.ntrace = 0;
+    e.greater = NONE;
+    e.gplay = 0;
+    e.cur = 0;
+    e.winner = NONE;
+}
+
+// ---- legal mask ------------------------------------------------------------------------------------------------
+struct Legal {
+    uint32_t total;   // legal combos (pass not included)
+    uint32_t nl;      // surviving dwords in L.list
+};
+
+__device__ __forceinline__ void zero_mask(WaveLds& L, int lane)
+{
+    uint4* z = (uint4*)L.mask;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int q = j * WAVE + lane;
+        if (q < MASK_WORDS / 4) z[q] = make_uint4(0, 0, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void test_pair(int da, int db, uint64_t h, const Cand& c, const Tab& tb, WaveLds& L,
+                                          int lane, Legal& r)
+{
+    const int d = lane < 32 ? da : db;
+    const uint32_t id = (uint32_t)d * 32u + (uint32_t)(lane & 31);
+    bool ok = false;
+    if (d >= 0 && id < (uint32_t)PASS) ok = contains(h, tb.cnt[id]) && c.ok(id);
+    const uint64_t m = __ballot(ok);
+    if (lane == 0) {
+        L.mask[MASK_PAD + da] = (uint32_t)m;
+        L.list[r.nl] = (uint16_t)da;
+        if (db >= 0) {
+            L.mask[MASK_PAD + db] = (uint32_t)(m >> 32);
+            L.list[r.nl + 1] = (uint16_t)db;
+        }
+    }
+    r.nl += db >= 0 ? 2u : 1u;
+    r.total += (uint32_t)__popcll(m);
+}
+
+// mask image must be zero on entry
+__device__ __forceinline__ Legal build_legal(const Env& e, const Cand& c, const Tab& tb, WaveLds& L, int lane)
+{
+    Legal r;
+    r.total = 0;
+    r.nl = 0;
+    if (e.over()) return r;                                        // game.py:110-128: no actions once over
+    const uint64_t h = e.hand(e.cur);
+    // a. groups
+    uint32_t base = 0;
+    const uint4* grp = (const uint4*)tb.grp;
+#pragma unroll
+    for (int k = 0; k < MAX_GROUPS / WAVE; k++) {
+        const int g = k * WAVE + lane;
+        bool pass = false;
+        if (g < tb.ng) {
+            const uint4 q = grp[g];
+            pass = contains(h, (uint64_t)q.x | ((uint64_t)q.y << 32)) && c.ok(q.z & 0xFFFFu);
+        }
+        const uint64_t b = __ballot(pass);
+        if (g <= tb.ng) L.pre[g] = (uint16_t)(base + mbcnt(b));
+        base += (uint32_t)__popcll(b);
+    }
+    if (base == 0) return r;
+    wave_sync_lds();
+    // b. dwords that any passing group overlaps, c. their ids, two dwords per wave pass
+    int pend = -1;
+    for (int k = 0; k < (ND + WAVE - 1) / WAVE; k++) {
+        const int d = k * WAVE + lane;
+        bool pass = false;
+        if (d < ND) {
+            const uint32_t dr = tb.drange[d];
+            pass = L.pre[(dr >> 16) + 1] > L.pre[dr & 0xFFFFu];
+        }
+        uint64_t bits = __ballot(pass);
+        while (bits) {
+            const int dd = k * WAVE + __builtin_ctzll(bits);
+            bits &= bits - 1;
+            if (pend < 0) {
+                pend = dd;
+            } else {
+                test_pair(pend, dd, h, c, tb, L, lane, r);
+                pend = -1;
+            }
+        }
+    }
+    if (pend >= 0) test_pair(pend, -1, h, c, tb, L, lane, r);
+    return r;
+}
+
+// the k-th legal id in ascending order (k < total + !leading; pass is the largest id)
+__device__ __forceinline__ uint32_t kth_legal(uint32_t k, const Legal& r, const WaveLds& L, int lane)
+{
+    if (k >= r.total) return (uint32_t)PASS;
+    for (uint32_t b0 = 0; b0 < r.nl; b0 += WAVE) {
+        const uint32_t i = b0 + (uint32_t)lane;
+        const uint32_t d = i < r.nl ? L.list[i] : 0u;
+        const uint32_t w = i < r.nl ? L.mask[MASK_PAD + d] : 0u;
+        const uint32_t pc = (uint32_t)__popc(w);
+        uint32_t inc = pc;
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+            if (lane >= o) inc += y;
+        }
+        const uint32_t tot = rl(inc, WAVE - 1);
+        if (k < tot) {
+            const int j = __builtin_ctzll(__ballot(inc > k));
+            uint32_t word = rl(w, j);
+            uint32_t kk = k - (rl(inc, j) - rl(pc, j));
+            while (kk--) word &= word - 1;
+            return rl(d, j) * 32u + (uint32_t)__builtin_ctz(word);
+        }
+        k -= tot;
+    }
+    return (uint32_t)PASS;   // unreachable
+}
+
+// ---- obs -------------------------------------------------------------------------------------------------------
+// _extract_state (envs/doudizhu.py:26-134) of player `self` as bits in L.bv. Blocks of 54 bits:
+//   0 hand, 1 others' cards, 2 last non-pass action, 3..11 the last 9 actions ('' padded in front), then
+//   landlord: 12 / 13 cards played by players 2 / 1, one-hots of their hand sizes at 756 / 773 (17 wide);
+//   peasant:  12 / 13 cards played by the landlord / teammate, 14 / 15 their last actions, one-hots of their hand
+//             sizes at 864 (20 wide) / 884 (17 wide).
+__device__ __forceinline__ void build_obs(const Env& e, uint32_t self, const Tab& tb, WaveLds& L, int lane)
+{
+    const uint32_t nt = e.ntrace;
+    const uint32_t h8 = e.hw4 & 0xFFFFu, h7 = e.hw3 >> 16, h6 = e.hw3 & 0xFFFFu;
+    uint32_t last = h8;
+    if (last == (uint32_t)PASS) last = h7;
+    const uint32_t mate = 3u - self;
+    uint32_t ll = NO_ACTION, lt = NO_ACTION;
+    if (self != 0) {
+        if (nt >= 1u) ll = (nt - 1u) % 3u == 0u ? h8 : ((nt - 1u) % 3u == 1u ? h7 : h6);
+        if (nt > mate) {
+            const uint32_t d = (nt - 1u - mate) % 3u;
+            lt = d == 0u ? h8 : (d == 1u ? h7 : h6);
+        }
+    }
+    const int s = lane;
+    uint32_t id = NO_ACTION;
+    uint64_t direct = 0;
+    if (s == 0) direct = e.hand(self);
+    else if (s == 1) direct = e.hand(self == 0 ? 1u : 0u) + e.hand(self == 2 ? 1u : 2u);
+    else if (s == 2) id = last;
+    else if (s <= 11) id = e.hist((uint32_t)(s - 3)); else if (s == 12) direct = self == 0 ? e.q2 : e.q0;
+    else if (s == 13) direct = self == 0 ? e.q1 : e.played(mate);
+    else if (s == 14 && self != 0) id = ll;
+    else if (s == 15 && self != 0) id = lt;
+    if (id < (uint32_t)PASS) direct = tb.cnt[id];
+    if (s < NSEG) L.segv[s] = cards_bits(direct);
+    uint32_t p1, p2;
+    if (self == 0) {
+        const uint32_t n2 = num_cards(e.h2), n1 = num_cards(e.h1);
+        p1 = 756u + (n2 >= 1u ? n2 - 1u : 16u);
+        p2 = 773u + (n1 >= 1u ? n1 - 1u : 16u);
+    } else {
+        const uint32_t n0 = num_cards(e.h0), nm = num_cards(e.hand(mate));
+        p1 = 864u + (n0 >= 1u ? n0 - 1u : 19u);
+        p2 = 884u + (nm >= 1u ? nm - 1u : 16u);
+    }
+    wave_sync_lds();
+    if (lane < BV_WORDS) {
+        const int x0 = lane == 0 ? 0 : 32 * lane - 16;             // first obs bit of this dword (lane 0: see below)
+        const int sg = x0 / 54, off = x0 - 54 * sg;
+        uint32_t v = (uint32_t)((L.segv[sg] >> off) | (L.segv[sg + 1] << (54 - off)));
+        if (lane == 0) v <<= 16;                                    // dword 0 = 16 pad bits + obs bits 0..15
+        const uint32_t d1 = p1 - (uint32_t)x0, d2 = p2 - (uint32_t)x0;
+        if (lane != 0) {
+            if (d1 < 32u) v |= 1u << d1;
+            if (d2 < 32u) v |= 1u << d2;
+        }
+        L.bv[lane] = v;
+    }
+}
+
+// ---- row writers: 16-B stores for the chunks fully inside the row, byte stores at its two ends ------------------
+__device__ __forceinline__ uint4 expand_bits16(uint32_t x)   // 16 bits -> 16 bytes of 0/1
+{
+    uint4 o;
+    o.x = ((x & 15u) * 0x00204081u) & 0x01010101u;
+    o.y = (((x >> 4) & 15u) * 0x00204081u) & 0x01010101u;
+    o.z = (((x >> 8) & 15u) * 0x00204081u) & 0x01010101u;
+    o.w = (((x >> 12) & 15u) * 0x00204081u) & 0x01010101u;
+    return o;
+}
+
+__device__ __forceinline__ void store_chunk(uint8_t* dst_al, int o, int nbytes, const uint4& v)
+{
+    if (o >= 0 && o + 16 <= nbytes) {
+        *(uint4*)dst_al = v;
+    } else {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            if (o + k >= 0 && o + k < nbytes) dst_al[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    }
+}
+
+__device__ __forceinline__ void write_obs_row(const WaveLds& L, uint8_t* row, int lane)
+{
+    const int mis = (int)((uintptr_t)row & 15u);
+    uint8_t* al = row - mis;
+    const int nchunks = (mis + OBS + 15) >> 4;                       // <= 58
+    if (lane < nchunks) {
+        const int o = 16 * lane - mis;                               // row byte of the chunk's first byte
+        const int bp = 16 + o;                                       // >= 1
+        const uint64_t two = (uint64_t)L.bv[bp >> 5] | ((uint64_t)L.bv[(bp >> 5) + 1] << 32);
+        store_chunk(al + 16 * lane, o, OBS, expand_bits16((uint32_t)(two >> (bp & 31)) & 0xFFFFu));
+    }
+}
+
+__device__ __forceinline__ void write_legal_row(const WaveLds& L, uint8_t* row, int lane)
+{
+    const int mis = (int)((uintptr_t)row & 15u);
+    uint8_t* al = row - mis;
+    const int nchunks = (mis + LB + 15) >> 4;                        // <= 216
+    const uint8_t* img = (const uint8_t*)L.mask + 4 * MASK_PAD;      // row byte b at img[b]
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int qn = j * WAVE + lane;
+        if (qn < nchunks) {
+            const int o = 16 * qn - mis;
+            const int sb = 4 * MASK_PAD + o;                             // byte offset into L.mask, >= 1
+            const uint32_t* w = L.mask + (sb >> 2);
+            const int sh = sb & 3;
+            uint4 v;
+            if (sh == 0) {
+                v = make_uint4(w[0], w[1], w[2], w[3]);
+            } else {
+                const uint32_t w4 = w[4];
+                v.x = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+                v.y = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
+                v.z = __builtin_amdgcn_alignbyte(w[3], w[2], sh);
+                v.w = __builtin_amdgcn_alignbyte(w4, w[3], sh);
+            }
+            store_chunk(al + 16 * qn, o, LB, v);
+        }
+    }
+    (void)img;
+}
+
+struct Ctx {
+    int lane, wid;
+    int64_t env;
+    bool valid;
+};
+__device__ __forceinline__ Ctx ctx_of(int64_t n)
+{
+    Ctx c;
+    c.lane = (int)(threadIdx.x & (WAVE - 1));
+    c.wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+    c.env = (int64_t)blockIdx.x * WPB + c.wid;
+    c.valid = c.env < n;
+    return c;
+}
+
+__device__ __forceinline__ WaveMt wave_mt(uint32_t* mt, const uint32_t* ctl, int64_t env)
+{
+    WaveMt m;
+    m.base = mt + env * MT_WORDS;
+    const uint32_t w = ctl[env];
+    m.pos = w & 0x7FFu;
+    m.stale = (w >> 16) & 1u;
+    return m;
+}
+
+// obs / legal / player / done of the current state, for `self` (observe) or the current player
+__device__ __forceinline__ void emit_state(const Env& e, uint32_t self, const Tab& tb, WaveLds& L, int lane,
+                                           int64_t row, const cs_step_out& out)
+{
+    zero_mask(L, lane);
+    wave_sync_lds();
+    const Cand cd = cand_of(e, tb);
+    build_legal(e, cd, tb, L, lane);
+    if (!e.over() && !cd.leading && lane == 0) L.mask[MASK_PAD + PASS / 32] |= 1u << (PASS & 31);
+    build_obs(e, self, tb, L, lane);
+    wave_sync_lds();
+    if (out.obs) write_obs_row(L, (uint8_t*)out.obs + row * OBS, lane);
+    if (out.legal) write_legal_row(L, (uint8_t*)out.legal + row * LB, lane);
+    if (lane == 0) {
+        if (out.player) ((uint8_t*)out.player)[row] = (uint8_t)e.cur;
+        if (out.done) ((uint8_t*)out.done)[row] = (uint8_t)e.over();
+    }
+}
+
+__device__ __forceinline__ void payoffs(const Env& e, float* r)   // judger.py:350-359
+{
+    r[0] = e.winner == 0 ? 1.f : 0.f;
+    r[1] = e.winner == 0 ? 0.f : 1.f;
+    r[2] = r[1];
+}
+
+__global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
+                                                  cs_step_out out, Tab tb)
+{
+    __shared__ WaveLds lds[WPB];
+    const Ctx c = ctx_of(n);
+    if (!c.valid) return;
+    WaveLds& L = lds[c.wid];
+    Env e;
+    WaveMt m = wave_mt(mt, ctl, c.env);
+    deal(e, m, c.lane);
+    emit_state(e, e.cur, tb, L, c.lane, c.env, out);
+    if (c.lane == 0 && out.reward) {
+        float* r = (float*)out.reward + c.env * P;
+        r[0] = r[1] = r[2] = 0.f;
+    }
+    e.store(st, c.env, c.lane);
+    if (c.lane == 0) ctl[c.env] = m.pos | (m.stale << 16);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
+                                                 const int32_t* actions, cs_step_out out, Tab tb)
+{
+    __shared__ WaveLds lds[WPB];
+    const Ctx c = ctx_of(n);
+    if (!c.valid) return;
+    WaveLds& L = lds[c.wid];
+    Env e;
+    e.load(st, c.env, c.lane);
+    WaveMt m = wave_mt(mt, ctl, c.env);
+    float r[3] = {0.f, 0.f, 0.f};
+    bool done = false;
+    if (e.over()) {
+        deal(e, m, c.lane);
+    } else {
+        const Cand cd = cand_of(e, tb);
+        e.apply(decode_action(actions[c.env], e, cd, tb), tb);
+        done = e.over();
+        if (done) payoffs(e, r);
+    }
+    emit_state(e, e.cur, tb, L, c.lane, c.env, out);
+    if (c.lane == 0) {
+        if (out.reward) {
+            float* o = (float*)out.reward + c.env * P;
+            o[0] = r[0]; o[1] = r[1]; o[2] = r[2];
+        }
+        if (out.done) ((uint8_t*)out.done)[c.env] = (uint8_t)done;
+    }
+    e.store(st, c.env, c.lane);
+    if (c.lane == 0) ctl[c.env] = m.pos | (m.stale << 16);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n, int player, cs_step_out out, Tab tb)
+{
+    __shared__ WaveLds lds[WPB];
+    const Ctx c = ctx_of(n);
+    if (!c.valid) return;
+    Env e;
+    e.load(st, c.env, c.lane);
+    emit_state(e, (uint32_t)player, tb, lds[c.wid], c.lane, c.env, out);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n, int T,
+                                                    uint64_t seed, uint64_t t0, uint64_t env_base, cs_traj_out out,
+                                                    Tab tb)
+{
+    __shared__ WaveLds lds[WPB];
+    const Ctx c = ctx_of(n);
+    if (!c.valid) return;
+    WaveLds& L = lds[c.wid];
+    const int lane = c.lane;
+    Env e;
+    e.load(st, c.env, lane);
+    WaveMt m = wave_mt(mt, ctl, c.env);
+    if (e.over()) deal(e, m, lane);
+    const uint64_t genv = env_base + (uint64_t)c.env;
+    for (int t = 0; t < T; t++) {
+        const int64_t row = (int64_t)t * n + c.env;
+        zero_mask(L, lane);
+        wave_sync_lds();
+        const Cand cd = cand_of(e, tb);
+        const Legal lg = build_legal(e, cd, tb, L, lane);
+        build_obs(e, e.cur, tb, L, lane);
+        wave_sync_lds();
+        const uint32_t count = lg.total + (cd.leading ? 0u : 1u);
+        const uint32_t rr = philox_u32(seed, genv, t0 + (uint64_t)t);
+        const uint32_t a = kth_legal((uint32_t)(((uint64_t)rr * count) >> 32), lg, L, lane);
+        if (!cd.leading && lane == 0) L.mask[MASK_PAD + PASS / 32] |= 1u << (PASS & 31);
+        wave_sync_lds();
+        write_obs_row(L, (uint8_t*)out.obs + row * OBS, lane);
+        write_legal_row(L, (uint8_t*)out.legal + row * LB, lane);
+        const uint32_t p = e.cur;
+        e.apply(a, tb);
+        const bool done = e.over();
+        if (lane == 0) {
+            ((uint8_t*)out.player)[row] = (uint8_t)p;
+            ((int16_t*)out.action)[row] = (int16_t)a;
+            float r[3] = {0.f, 0.f, 0.f};
+            if (done) payoffs(e, r);
+            float* o = (float*)out.reward + row * P;
+            o[0] = r[0]; o[1] = r[1]; o[2] = r[2];
+            ((uint8_t*)out.done)[row] = (uint8_t)done;
+        }
+        if (done) deal(e, m, lane);
+    }
+    e.store(st, c.env, lane);
+    if (lane == 0) ctl[c.env] = m.pos | (m.stale << 16);
+}
+
+static inline dim3 grid_of(int64_t n) { return dim3((unsigned)((n + WPB - 1) / WPB)); }
+
+hipError_t launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_reset, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, o, *(const Tab*)b.table);
+    return hipGetLastError();
+}
+hipError_t launch_step(const Buffers& b, const int32_t* a, const cs_step_out& o, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_step, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, a, o,
+                       *(const Tab*)b.table);
+    return hipGetLastError();
+}
+hipError_t launch_observe(const Buffers& b, int32_t p, const cs_step_out& o, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_observe, grid_of(b.n), dim3(BLOCK), 0, s, b.state, b.n, p, o, *(const Tab*)b.table);
+    return hipGetLastError();
+}
+hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
+                          const cs_traj_out& o, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_rollout, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0, env_base, o,
+                       *(const Tab*)b.table);
+    return hipGetLastError();
+}
+
+}  // namespace ddz
+}  // namespace cs

@@ -13,7 +13,7 @@ struct Buffers {
     int64_t n;
     uint32_t* mt;     // [n][1248]
     uint32_t* ctl;    // [n]
-    uint32_t* state;  // [state_words][n]
+    uint32_t* state;  // [state_words][n] (lane-per-env games) or [n][state_words] (doudizhu, wave per env)
     uint32_t* sctl;   // [n] rollout MT staging: staged stream position | staged count << 16
     uint8_t* sbuf;    // [n][stage bytes] rollout MT staging rows persisted between launches
     const void* table;  // game-specific read-only table (doudizhu action table), or null
@@ -23,6 +23,7 @@ struct Buffers {
 
 int game_info(int32_t game, const cs_config* cfg, cs_game_info* info);
 int64_t stage_bytes_per_env(int32_t game, int32_t num_players);
+inline bool state_env_major(int32_t game) { return game == CS_GAME_DOUDIZHU; }
 
 hipError_t launch_seed(const Buffers& b, const uint32_t* keys_dev, const int32_t* klen_dev, int64_t first,
                        int64_t count, hipStream_t s);
@@ -31,5 +32,13 @@ hipError_t launch_step(const Buffers& b, const int32_t* actions, const cs_step_o
 hipError_t launch_observe(const Buffers& b, int32_t player, const cs_step_out& o, hipStream_t s);
 hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
                           const cs_traj_out& o, hipStream_t s);
+
+namespace ddz {   // cs_doudizhu.hip (seeding goes through the shared k_seed)
+hipError_t launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s);
+hipError_t launch_step(const Buffers& b, const int32_t* actions, const cs_step_out& o, hipStream_t s);
+hipError_t launch_observe(const Buffers& b, int32_t player, const cs_step_out& o, hipStream_t s);
+hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
+                          const cs_traj_out& o, hipStream_t s);
+}  // namespace ddz
 
 }  // namespace cs

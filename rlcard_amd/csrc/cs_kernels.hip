@@ -9,6 +9,7 @@
 #include "cs_leduc.h"
 #include "cs_limit.h"
 #include "cs_blackjack.h"
+#include "cs_doudizhu.h"
 
 namespace cs {
 
@@ -460,6 +461,15 @@ int game_info(int32_t game, const cs_config* cfg, cs_game_info* info)
         else fill_info<Blackjack<4>>(info);
         return CS_OK;
     }
+    case CS_GAME_DOUDIZHU:
+        if (cfg && cfg->num_players != 0 && cfg->num_players != ddz::P) return CS_E_UNSUPPORTED;
+        info->obs_dim = ddz::OBS;
+        info->num_actions = ddz::NA;
+        info->num_players = ddz::P;
+        info->legal_bytes = ddz::LB;
+        info->action_bytes = 2;
+        info->state_words = ddz::WORDS;
+        return CS_OK;
     default:
         return CS_E_UNSUPPORTED;
     }
@@ -483,24 +493,28 @@ hipError_t launch_seed(const Buffers& b, const uint32_t* keys, const int32_t* kl
                        hipStream_t s)
 {
 #define C_(G) seed_g<G>(b, keys, klen, first, count, s)
+    if (b.game == CS_GAME_DOUDIZHU) return C_(ddz::SeedView);
     CS_DISPATCH(b.game, C_)
 #undef C_
 }
 hipError_t launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s)
 {
 #define C_(G) reset_g<G>(b, o, s)
+    if (b.game == CS_GAME_DOUDIZHU) return ddz::launch_reset(b, o, s);
     CS_DISPATCH(b.game, C_)
 #undef C_
 }
 hipError_t launch_step(const Buffers& b, const int32_t* a, const cs_step_out& o, hipStream_t s)
 {
 #define C_(G) step_g<G>(b, a, o, s)
+    if (b.game == CS_GAME_DOUDIZHU) return ddz::launch_step(b, a, o, s);
     CS_DISPATCH(b.game, C_)
 #undef C_
 }
 hipError_t launch_observe(const Buffers& b, int32_t p, const cs_step_out& o, hipStream_t s)
 {
 #define C_(G) observe_g<G>(b, p, o, s)
+    if (b.game == CS_GAME_DOUDIZHU) return ddz::launch_observe(b, p, o, s);
     CS_DISPATCH(b.game, C_)
 #undef C_
 }
@@ -508,6 +522,7 @@ hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t
                           const cs_traj_out& o, hipStream_t s)
 {
 #define C_(G) rollout_g<G>(b, T, seed, t0, env_base, o, s)
+    if (b.game == CS_GAME_DOUDIZHU) return ddz::launch_rollout(b, T, seed, t0, env_base, o, s);
     CS_DISPATCH(b.game, C_)
 #undef C_
 }

@@ -25,10 +25,23 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_game_info_shapes():
-    shapes = {'leduc-holdem': (36, 4, 2, 1), 'limit-holdem': (72, 4, 2, 1), 'blackjack': (2, 2, 1, 1)}
-    for game, (o, a, p, lb) in shapes.items():
+    shapes = {'leduc-holdem': (36, 4, 2, 1, 1), 'limit-holdem': (72, 4, 2, 1, 1), 'blackjack': (2, 2, 1, 1, 1),
+              'doudizhu': (901, 27472, 3, 3434, 2)}
+    for game, (o, a, p, lb, ab) in shapes.items():
         info, _ = _abi.game_info(game)
-        assert (info.obs_dim, info.num_actions, info.num_players, info.legal_bytes) == (o, a, p, lb)
+        assert (info.obs_dim, info.num_actions, info.num_players, info.legal_bytes, info.action_bytes) == \
+            (o, a, p, lb, ab)
+
+
+def test_doudizhu_action_table_is_compiled_in():
+    """The .incbin'd table is the one tools/gen_ddz_table.py derives from the reference capture."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location('gen_ddz_table', os.path.join(ROOT, 'tools', 'gen_ddz_table.py'))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    blob = g.build(os.path.join(ROOT, 'tests', 'golden', 'ddz_actions.npz'))
+    assert open(os.path.join(ROOT, 'rlcard_amd', 'csrc', 'ddz_actions.bin'), 'rb').read() == blob
+    assert blob in open(_abi.LIB_PATH, 'rb').read()
 
 
 def test_create_fails_loudly_without_gpu():

@@ -1,0 +1,49 @@
+"""Writes rlcard_amd/csrc/ddz_actions.bin, the DouDizhu action-id table compiled into libcardsim.so (.incbin).
+
+Source: tests/golden/ddz_actions.npz (captured from the reference's action space, rlcard/games/doudizhu/jsondata.zip
+via rlcard/envs/doudizhu.py:20-21 and rlcard/games/doudizhu/utils.py:14-38; see tests/golden/gen_golden.py).
+Format (little endian):
+  'DDZT', u32 num_actions, u32 pass_id, u32 reserved
+  u64 counts[num_actions]   rank counts packed as nibbles: rank r (3..A,2,B,R = 0..14) at bits 4r..4r+3; pass = 0
+  u8  type[num_actions]     index into TYPE_NAMES below; pass = 255
+  u8  weight[num_actions]   the reference's type-local weight (pass = 0)
+Run: python3 tools/gen_ddz_table.py
+"""
+import os
+import struct
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TYPE_NAMES = ['solo'] + ['solo_chain_%d' % k for k in range(5, 13)] + ['pair'] + \
+    ['pair_chain_%d' % k for k in range(3, 11)] + ['trio'] + ['trio_chain_%d' % k for k in range(2, 7)] + \
+    ['trio_solo'] + ['trio_solo_chain_%d' % k for k in range(2, 6)] + ['trio_pair'] + \
+    ['trio_pair_chain_%d' % k for k in range(2, 5)] + ['four_two_solo', 'four_two_pair', 'bomb', 'rocket']
+
+
+def build(npz_path):
+    d = np.load(npz_path)
+    names = [str(x) for x in d['type_names']]
+    assert names == TYPE_NAMES, 'type table order changed'
+    counts, typ, weight, pass_id = d['counts'], d['type'], d['weight'], int(d['pass_id'])
+    na = counts.shape[0]
+    assert counts.shape == (na, 15) and counts.max() <= 4 and pass_id == na - 1
+    packed = np.zeros(na, np.uint64)
+    for r in range(15):
+        packed |= counts[:, r].astype(np.uint64) << np.uint64(4 * r)
+    t = typ.astype(np.int64)
+    t[pass_id] = 255
+    w = weight.astype(np.int64)
+    w[pass_id] = 0
+    assert t.min() >= 0 and t.max() <= 255 and w.min() >= 0 and w.max() < 256
+    return (b'DDZT' + struct.pack('<III', na, pass_id, 0) + packed.astype('<u8').tobytes()
+            + t.astype(np.uint8).tobytes() + w.astype(np.uint8).tobytes())
+
+
+if __name__ == '__main__':
+    blob = build(os.path.join(ROOT, 'tests', 'golden', 'ddz_actions.npz'))
+    out = os.path.join(ROOT, 'rlcard_amd', 'csrc', 'ddz_actions.bin')
+    with open(out, 'wb') as f:
+        f.write(blob)
+    print('wrote %s (%d bytes)' % (out, len(blob)), file=sys.stderr)
