@@ -7,3 +7,4 @@ on one GPU through the C ABI in include/cardsim.h (HIP kernels for gfx950, rlcar
 __version__ = '0.1.0'
 
 from .vec import VecEnv, legal_mask, legal_ids  # noqa: F401
+from .envs import make, register  # noqa: F401

@@ -1,0 +1,37 @@
+"""Blackjack env (rlcard/envs/blackjack.py:38-103) over the HIP engine (rlcard_amd/csrc/cs_blackjack.h)."""
+import numpy as np
+
+from .env import Env
+from .limitholdem import card_str
+
+
+class BlackjackEnv(Env):
+    name = 'blackjack'
+    default_game_config = {'game_num_players': 1, 'game_num_decks': 1}
+    configurable = True
+    actions = ['hit', 'stand']
+
+    def __init__(self, config):
+        super().__init__(config)
+        self.state_shape = [[2] for _ in range(self.num_players)]
+        self.action_shape = [None for _ in range(self.num_players)]
+
+    def _obs_of(self, obs_bytes, player_id):
+        return obs_bytes.astype(np.int64)          # (player score, dealer's visible score)
+
+    def _hands(self):
+        w = self._state_words()
+        sizes = w[30]
+        hands = []
+        for h in range(self.num_players + 1):
+            n = (sizes >> (4 * h)) & 15
+            hands.append([card_str((w[15 + (12 * h + k) // 4] >> (8 * ((12 * h + k) % 4))) & 255) for k in range(n)])
+        return hands
+
+    def _raw_obs(self, player_id, legal):
+        hands = self._hands()
+        dealer = hands[-1] if self.is_over() else hands[-1][1:]
+        return {'actions': tuple(self.actions), 'state': (hands[player_id], dealer)}
+
+    def _payoff_array(self, r):
+        return np.asarray(r, dtype=np.int64)        # blackjack.py get_payoffs: 1 win, 0 tie, -1 loss

@@ -1,0 +1,171 @@
+"""Single-env compatibility layer: rlcard's Env API (rlcard/envs/env.py:3-231) over one env of the HIP engine.
+
+An Env owns a VecEnv of size 1 on one GPU and keeps rlcard's host-side contract -- reset/step/run/get_state/
+get_payoffs/is_over/get_player_id/seed/timestep/action_recorder, state dicts {'obs', 'legal_actions', 'raw_obs',
+'raw_legal_actions', 'action_record'} with the reference's obs dtypes and shapes -- so code written against
+rlcard.make() runs unchanged. Every game rule, deal and observation is computed by the kernels; this layer only
+converts one row of the engine's outputs into the reference's Python types. Throughput belongs to VecEnv.
+"""
+from collections import OrderedDict
+
+import numpy as np
+
+from .. import seeding
+from ..vec import VecEnv, legal_ids
+
+
+class Env(object):
+    """Subclasses set name, default_game_config, actions, state_shape, action_shape and implement _obs_of /
+    _raw_obs / get_payoffs (the reference's _extract_state / get_payoffs split)."""
+    name = None
+    default_game_config = {}
+    configurable = False   # env.py:33-39: only blackjack / leduc / limit forward 'game_*' keys
+
+    def __init__(self, config):
+        self.allow_step_back = bool(config.get('allow_step_back', False))
+        game_config = dict(self.default_game_config)
+        if self.configurable:
+            for k in config:
+                if k in game_config:
+                    game_config[k] = config[k]
+        self.game_config = game_config
+        self.action_recorder = []
+        self.agents = None
+        self._vec = VecEnv(self.name, 1, seeds=[0], device=config.get('device'), config=game_config)
+        self.num_players = self._vec.num_players
+        self.num_actions = self._vec.num_actions
+        self.timestep = 0
+        self._last = None
+        self._payoffs = None
+        self.seed(config.get('seed'))
+
+    # -- rlcard Env API ----------------------------------------------------------------------------------------
+    def reset(self):
+        out = self._host(self._vec.reset())
+        self.action_recorder = []
+        self._payoffs = None
+        self._last = out
+        return self._extract_state(out, out['player']), out['player']
+
+    def step(self, action, raw_action=False):
+        if self._last is None:
+            raise RuntimeError('call reset() before step()')
+        a = self._action_id(action) if raw_action else int(action)
+        if not 0 <= a < self.num_actions:
+            raise ValueError('action id %d out of range [0, %d)' % (a, self.num_actions))
+        decoded = self._decode_action(a)
+        self.timestep += 1
+        self.action_recorder.append((self.get_player_id(), decoded))
+        out = self._host(self._vec.step(np.array([self._action_id(decoded)], dtype=np.int32)))
+        if out['done']:
+            self._payoffs = out['reward']
+        self._last = out
+        return self._extract_state(out, out['player']), out['player']
+
+    def step_back(self):
+        # Leduc/Limit CFR tree walking (game.py step_back) is not part of the lockstep engine
+        if not self.allow_step_back:
+            raise Exception('Step back is off. To use step_back, please set allow_step_back=True in rlcard.make')
+        raise NotImplementedError('step_back is not supported by the lockstep engine')
+
+    def set_agents(self, agents):
+        self.agents = agents
+
+    def run(self, is_training=False):
+        """env.py:120-169: one game, trajectories[p] = [state, action, state, ..., final state] + payoffs."""
+        trajectories = [[] for _ in range(self.num_players)]
+        state, player_id = self.reset()
+        trajectories[player_id].append(state)
+        while not self.is_over():
+            if not is_training:
+                action, _ = self.agents[player_id].eval_step(state)
+            else:
+                action = self.agents[player_id].step(state)
+            next_state, next_player_id = self.step(action, self.agents[player_id].use_raw)
+            trajectories[player_id].append(action)
+            state, player_id = next_state, next_player_id
+            if not self.is_over():
+                trajectories[player_id].append(state)
+        for p in range(self.num_players):
+            trajectories[p].append(self.get_state(p))
+        return trajectories, self.get_payoffs()
+
+    def is_over(self):
+        return bool(self._last is not None and self._last['done'])
+
+    def get_player_id(self):
+        return int(self._last['player'])
+
+    def get_state(self, player_id):
+        o = self._vec.observe(player_id)
+        out = {k: v[0].cpu().numpy() for k, v in o.items()}
+        out['player'] = int(out['player'])
+        out['done'] = bool(out['done'])
+        return self._extract_state(out, player_id)
+
+    def get_payoffs(self):
+        r = self._payoffs if self._payoffs is not None else np.zeros(self.num_players, np.float32)
+        return self._payoff_array(r)
+
+    def get_perfect_information(self):
+        raise NotImplementedError
+
+    def get_action_feature(self, action):
+        feature = np.zeros(self.num_actions, dtype=np.int8)
+        feature[action] = 1
+        return feature
+
+    def seed(self, seed=None):
+        """env.py:228-231 + utils/seeding.py: same seed -> same init_by_array key -> same deals."""
+        s = seeding.create_seed(seed)
+        self._vec.seed([s])
+        self._last = None
+        return s
+
+    # -- engine row -> reference types ---------------------------------------------------------------------------
+    @staticmethod
+    def _host(o):
+        out = {k: v[0].cpu().numpy() for k, v in o.items()}
+        out['player'] = int(out['player'])
+        out['done'] = bool(out['done'])
+        return out
+
+    def _legal_ids(self, out):
+        return legal_ids(out['legal'])
+
+    def _extract_state(self, out, player_id):
+        ids = self._legal_ids(out)
+        state = {
+            'legal_actions': OrderedDict((i, self._legal_value(i)) for i in ids),
+            'obs': self._obs_of(out['obs'], player_id),
+            'raw_obs': self._raw_obs(player_id, ids),
+            'raw_legal_actions': [self._raw_action(i) for i in ids],
+            'action_record': self.action_recorder,
+        }
+        return state
+
+    def _legal_value(self, action_id):
+        return None
+
+    def _raw_action(self, action_id):
+        return self.actions[action_id]
+
+    def _action_id(self, raw):
+        if isinstance(raw, (int, np.integer)):
+            return int(raw)
+        return self.actions.index(raw)
+
+    def _decode_action(self, action_id):
+        return self._raw_action(action_id)
+
+    def _obs_of(self, obs_bytes, player_id):
+        return obs_bytes.astype(np.float64)
+
+    def _raw_obs(self, player_id, legal):
+        return None
+
+    def _payoff_array(self, r):
+        return np.asarray(r, dtype=np.float64)
+
+    def _state_words(self):
+        return self._vec.env_state_words(0)

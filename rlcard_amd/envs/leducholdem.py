@@ -1,0 +1,42 @@
+"""Leduc Hold'em env (rlcard/envs/leducholdem.py:11-112) over the HIP engine (rlcard_amd/csrc/cs_leduc.h)."""
+import numpy as np
+
+from .env import Env
+
+CARDS = ['SJ', 'HJ', 'SQ', 'HQ', 'SK', 'HK']   # engine card index = rlcard/games/leducholdem/dealer.py deck order
+
+
+class LeducholdemEnv(Env):
+    name = 'leduc-holdem'
+    default_game_config = {'game_num_players': 2}
+    configurable = True
+    actions = ['call', 'raise', 'fold', 'check']
+
+    def __init__(self, config):
+        super().__init__(config)
+        self.state_shape = [[36] for _ in range(self.num_players)]
+        self.action_shape = [None for _ in range(self.num_players)]
+
+    def _decode_action(self, action_id):
+        """leducholdem.py:81-96: an illegal id becomes check, else fold."""
+        legal = self._legal_ids(self._last)
+        if action_id not in legal:
+            return 'check' if 3 in legal else 'fold'
+        return self.actions[action_id]
+
+    def _fields(self):
+        w0, w1 = self._state_words()
+        return dict(h=[w0 & 7, (w0 >> 3) & 7], pub=(w0 >> 6) & 7, chips=[(w0 >> 9) & 31, (w0 >> 14) & 31],
+                    rc=w1 & 3, ptr=(w1 >> 2) & 1)
+
+    def _raw_obs(self, player_id, legal):
+        f = self._fields()
+        return {'hand': CARDS[f['h'][player_id]], 'public_card': CARDS[f['pub']] if f['rc'] >= 1 else None,
+                'all_chips': f['chips'], 'my_chips': f['chips'][player_id],
+                'legal_actions': [self.actions[i] for i in legal], 'current_player': f['ptr']}
+
+    def get_perfect_information(self):
+        f = self._fields()
+        return {'chips': f['chips'], 'public_card': CARDS[f['pub']] if f['rc'] >= 1 else None,
+                'hand_cards': [CARDS[h] for h in f['h']], 'current_round': f['rc'], 'current_player': f['ptr'],
+                'legal_actions': [self.actions[i] for i in self._legal_ids(self._last)]}

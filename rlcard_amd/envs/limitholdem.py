@@ -1,0 +1,47 @@
+"""Limit Texas Hold'em env (rlcard/envs/limitholdem.py:40-96) over the HIP engine (rlcard_amd/csrc/cs_limit.h)."""
+import numpy as np
+
+from .env import Env
+
+
+def card_str(c):   # card2index order: S A..K = 0..12, H, D, C
+    return 'SHDC'[c // 13] + 'A23456789TJQK'[c % 13]
+
+
+class LimitholdemEnv(Env):
+    name = 'limit-holdem'
+    default_game_config = {'game_num_players': 2}
+    configurable = True
+    actions = ['call', 'raise', 'fold', 'check']
+
+    def __init__(self, config):
+        super().__init__(config)
+        self.state_shape = [[72] for _ in range(self.num_players)]
+        self.action_shape = [None for _ in range(self.num_players)]
+
+    def _decode_action(self, action_id):
+        """limitholdem.py:81-96: an illegal id becomes check, else fold."""
+        legal = self._legal_ids(self._last)
+        if action_id not in legal:
+            return 'check' if 3 in legal else 'fold'
+        return self.actions[action_id]
+
+    def _fields(self):
+        w0, w1, w2, w3 = self._state_words()
+        rc = (w2 >> 21) & 7
+        nboard = 0 if rc == 0 else min(5, rc + 2)
+        return dict(hands=[[w0 & 63, (w0 >> 6) & 63], [(w0 >> 12) & 63, (w0 >> 18) & 63]],
+                    board=[(w1 >> (6 * k)) & 63 for k in range(nboard)], chips=[(w0 >> 24) & 63, w2 & 63],
+                    ptr=(w0 >> 30) & 1, rc=rc, raise_nums=[(w3 >> (3 * k)) & 7 for k in range(4)])
+
+    def _raw_obs(self, player_id, legal):
+        f = self._fields()
+        return {'hand': [card_str(c) for c in f['hands'][player_id]], 'public_cards': [card_str(c) for c in f['board']],
+                'all_chips': f['chips'], 'my_chips': f['chips'][player_id],
+                'legal_actions': [self.actions[i] for i in legal], 'raise_nums': f['raise_nums']}
+
+    def get_perfect_information(self):
+        f = self._fields()
+        return {'chips': f['chips'], 'public_card': [card_str(c) for c in f['board']],
+                'hand_cards': [[card_str(c) for c in h] for h in f['hands']], 'current_round': f['rc'],
+                'current_player': f['ptr'], 'legal_actions': [self.actions[i] for i in self._legal_ids(self._last)]}

@@ -4,7 +4,7 @@ Mirrors rlcard/utils/seeding.py:33-113: an int seed is reduced mod 2**64 (create
 sha512(str(seed)) and the first 8 bytes read as a little-endian integer (hash_seed, :51-73 and _bigint_from_bytes,
 :99-108), which is split into little-endian u32 words with trailing zero words dropped (_int_list_from_bigint,
 :110-121; 0 -> [0]). numpy's RandomState.seed(list) then runs init_by_array over those words; the device does the
-same (rlcard_amd/csrc/mt19937.h). ``seed=None`` draws the seed from os.urandom like the reference.
+same (mt_init_by_array, rlcard_amd/csrc/cs_kernels.hip). ``seed=None`` draws the seed from os.urandom like the reference.
 """
 import hashlib
 import os
