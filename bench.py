@@ -77,7 +77,7 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from rlcard_amd import VecEnv
+    from rlcard_amd.shard import ShardedVecEnv, gather_traj, new_gathered
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -95,12 +95,10 @@ def main():
 
     game, T = args.game, args.T
     N = args.envs or GAMES[game]['envs']
-    env = VecEnv(game, N, seed=42, env_base=rank * N, device=local)
+    env = ShardedVecEnv(game, N, rank, seed=42, device=local)   # global envs [rank*N, (rank+1)*N)
     env.reset()
     traj = env.new_traj_out(T)
-    gathered = None
-    if args.gather and world > 1:
-        gathered = {k: torch.empty((world,) + v.shape, dtype=v.dtype, device=v.device) for k, v in traj.items()}
+    gathered = new_gathered(traj, world) if args.gather and world > 1 else None
 
     stream = torch.cuda.current_stream()
     t_launch = 0
@@ -131,8 +129,7 @@ def main():
         for k in range(args.steps):
             env.rollout(T, policy_seed=5, t0=t_launch * T, out=traj)
             t_launch += 1
-            for key, v in traj.items():
-                dist.all_gather_into_tensor(gathered[key], v)
+            gather_traj(traj, gathered)
         torch.cuda.synchronize()
         barrier()
         gel = time.perf_counter() - g0

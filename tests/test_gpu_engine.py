@@ -186,3 +186,20 @@ def test_full_size_rollout_properties_and_sampled_parity(oracle, game, name):
         exp = ob.rollout(T, 5, 0, start)
         got = {k: x[:, start:start + win].cpu().numpy() for k, x in tr.items()}
         _assert_same(got, exp, 'window %d' % start)
+
+
+@pytest.mark.parametrize('game,name', GAMES)
+def test_env_shards_equal_one_gpu_run(game, name):
+    """bench.py's multi-GPU layout on one GPU: two shards (env_base 0 and n) reproduce a single 2n-env run."""
+    from rlcard_amd.shard import ShardedVecEnv
+    n, T = (64, 8) if game == 'doudizhu' else (1000, 16)
+    full = _vec(game, 2 * n, seed=42)
+    full.reset()
+    ref = [_np(full.rollout(T, policy_seed=5, t0=c * T)) for c in range(2)]
+    shards = [ShardedVecEnv(game, n, r, seed=42) for r in range(2)]
+    for s in shards:
+        s.reset()
+    for c in range(2):
+        parts = [_np(s.rollout(T, policy_seed=5, t0=c * T)) for s in shards]
+        for k in ref[c]:
+            assert np.array_equal(np.concatenate([p[k] for p in parts], axis=1), ref[c][k]), (c, k)

@@ -1,0 +1,68 @@
+"""Multi-rank layout on CPU (gloo, world size 2): rank r replays its env shard [r*N, (r+1)*N) -- seeds 42 + global
+id, policy counter on the global id -- and the gathered trajectory equals one process running all 2N envs. The
+producer here is the CPU oracle (test infrastructure); the shard arithmetic and the gather are the product's
+(rlcard_amd/shard.py, used by bench.py)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GAMES = [('leduc-holdem', 96, 24), ('limit-holdem', 64, 16), ('blackjack', 64, 16), ('doudizhu', 8, 8)]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _oracle_traj(game, env_base, n, T, chunks):
+    sys.path.insert(0, HERE)
+    import oracle_lib
+    from rlcard_amd import seeding
+    keys, lens = seeding.seed_keys(range(42 + env_base, 42 + env_base + n))
+    b = oracle_lib.Batch(game, n, keys, lens)
+    b.reset()
+    out = [b.rollout(T, 5, c * T, env_base) for c in range(chunks)]
+    return {k: np.concatenate([o[k] for o in out], 0) for k in out[0]}
+
+
+def _worker(rank, world, port, game, n, T, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from rlcard_amd.shard import shard_range, gather_traj, new_gathered
+        base, m = shard_range(n, rank)
+        mine = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in _oracle_traj(game, base, m, T, 2).items()}
+        got = gather_traj(mine, new_gathered(mine, world))
+        if rank == 0:
+            q.put({k: v.numpy() for k, v in got.items()})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('game,n,T', GAMES)
+def test_two_rank_shards_gather_to_the_single_process_trajectory(oracle, game, n, T):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, game, n, T, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full = _oracle_traj(game, 0, 2 * n, T, 2)
+    for k, v in full.items():
+        # gathered [world, T', n, ...] -> [T', world * n, ...]
+        g = np.concatenate([got[k][r] for r in range(2)], axis=1)
+        assert np.array_equal(g, v), k
