@@ -63,6 +63,17 @@ def cpu_baseline(game, budget_s=12.0):
                        'oracle/liboracle.so scalar C' % (game, n_s, 41 + n_s, steps // n_s, el))
 
 
+def measured_traffic(game, envs, T):
+    """HBM bytes per k_rollout launch of this configuration from the committed rocprofv3 PMC profile
+    (profiles/traffic.json, written by tools/pmc_traffic.py), or None."""
+    try:
+        with open(os.path.join(ROOT, 'profiles', 'traffic.json')) as f:
+            e = json.load(f).get('%s:%d:%d' % (game, envs, T))
+    except (OSError, ValueError):
+        return None
+    return e
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -174,6 +185,11 @@ def main():
                          'alg_bytes_per_env_step': B, 'kernel_ms_per_launch': kernel_ms,
                          'kernel': 'k_rollout<%s>' % game},
         }
+        tr = measured_traffic(game, N, T)
+        if tr is not None:   # per launch, like `achieved`; from the profile of this exact configuration
+            line['roofline']['traffic'] = tr['bytes_per_launch']
+            line['roofline']['traffic_source'] = tr['source']
+            line['roofline']['alg_bytes_per_launch'] = B * N * T
         if gather_info is not None:
             line['gather'] = gather_info
         if world == 1 and not args.no_cpu_baseline:
