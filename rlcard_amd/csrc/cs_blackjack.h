@@ -31,6 +31,7 @@ struct Blackjack {
     static constexpr bool RAW_OBS = true;      // observe() returns byte values, not a 0/1 bitmap
     static constexpr int SCRATCH_WORDS = WORDS;
     static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_R = 100;  // MT staging (see MtLaneT)
+    static constexpr int RESTAGE_B = 8;  // lanes restaged per pass (loads in flight), measured: 8 > 4 > 1
     static constexpr int HAND_CAP = 12;
 
     uint32_t* s;   // lane scratch: word i at s[i * WAVE]

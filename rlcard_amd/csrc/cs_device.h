@@ -225,18 +225,68 @@ struct MtLaneT {
 };
 using MtLane = MtLaneT<STAGE_NONE>;
 
-// End-of-step convergence point: the wave refills every stale block of its lanes. All 64 lanes must call this.
+// dst[s] = twist(src[s]) for K streams at once, phases interleaved so the K twists' loads overlap (see mt_twist_wave)
+template <int K>
+__device__ __forceinline__ void mt_twist_wave_k(const uint32_t* const (&src)[K], uint32_t* const (&dst)[K], int lane)
+{
+    constexpr int H = MT_N - MT_M;  // 227
+    uint32_t n1[K][4], n2[K][4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const int k = 64 * c + lane;
+#pragma unroll
+        for (int s = 0; s < K; s++) n1[s][c] = k < H ? mt_mix(src[s][k], src[s][k + 1], src[s][k + MT_M]) : 0u;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const int k = 64 * c + lane;
+#pragma unroll
+        for (int s = 0; s < K; s++)
+            if (k < H) dst[s][k] = n1[s][c];
+    }
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const int k = H + 64 * c + lane;
+#pragma unroll
+        for (int s = 0; s < K; s++) n2[s][c] = k < 2 * H ? mt_mix(src[s][k], src[s][k + 1], n1[s][c]) : 0u;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const int k = H + 64 * c + lane;
+#pragma unroll
+        for (int s = 0; s < K; s++)
+            if (k < 2 * H) dst[s][k] = n2[s][c];
+    }
+#pragma unroll
+    for (int s = 0; s < K; s++) {
+        const uint32_t new0 = __builtin_amdgcn_readlane(n1[s][0], 0);
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const int k = 2 * H + 64 * c + lane;
+            if (k < MT_N - 1) dst[s][k] = mt_mix(src[s][k], src[s][k + 1], n2[s][c]);
+            else if (k == MT_N - 1) dst[s][k] = mt_mix(src[s][k], new0, n2[s][c]);
+        }
+    }
+}
+
+// End-of-step convergence point: the wave refills every stale block of its lanes, two lanes' twists at a time
+// (their loads overlap; an odd last lane is paired with itself: identical writes, harmless). All 64 lanes must call.
 template <class M>
 __device__ __forceinline__ void mt_refill_wave(M& m, int lane)
 {
     uint64_t need = __ballot(m.stale != 0);
     while (need) {
-        const int j = __builtin_ctzll(need);
+        const int j0 = __builtin_ctzll(need);
         need &= need - 1;
-        uint32_t* jb = lane_ptr(m.base, j);
-        const uint32_t jpos = __builtin_amdgcn_readlane(m.pos, j);
-        const uint32_t cur = jpos < MT_N ? 0 : MT_N;
-        mt_twist_wave(jb + cur, jb + (MT_N - cur), lane);
+        const int j1 = need ? __builtin_ctzll(need) : j0;
+        need &= need - 1;
+        uint32_t* b0 = lane_ptr(m.base, j0);
+        uint32_t* b1 = lane_ptr(m.base, j1);
+        const uint32_t c0 = __builtin_amdgcn_readlane(m.pos, j0) < MT_N ? 0 : MT_N;
+        const uint32_t c1 = __builtin_amdgcn_readlane(m.pos, j1) < MT_N ? 0 : MT_N;
+        const uint32_t* const src[2] = {b0 + c0, b1 + c1};
+        uint32_t* const dst[2] = {b0 + (MT_N - c0), b1 + (MT_N - c1)};
+        mt_twist_wave_k<2>(src, dst, lane);
     }
     m.stale = 0;
     // the refilled words are read later by their owner lane of this same wave: order the stores before those loads
@@ -264,32 +314,52 @@ __device__ __forceinline__ void wave_sync_lds()
 // loaded COALESCED by the whole wave (all 64 lanes read one lane's consecutive words), tempered and packed to bytes
 // (lanes 4q gather lanes 4q+1..3 with DPP row shifts: VALU, no LDS traffic). area = the wave's staging area (lane j's
 // row at area + j * STRIDE). All 64 lanes must call.
-template <int W, int R>
+template <int W, int R, int B>
 __device__ __forceinline__ void mt_restage_wave(MtLaneT<STAGE_LDS>& m, uint8_t* area, int lane)
 {
-    constexpr int STRIDE = Stage<W>::STRIDE;
+    constexpr int STRIDE = Stage<W>::STRIDE, C = W / WAVE;
     m.stg = area + lane * STRIDE;
     const uint32_t k = m.staged_offset();
     uint64_t todo = __ballot(k >= m.sn || m.sn - k < (uint32_t)R);
     while (todo) {
-        const int j = __builtin_ctzll(todo);
+        // B needy lanes per pass, all their loads issued before the first is used (a pass with fewer than B left
+        // repeats its first lane: same words, same bytes, harmless)
+        int js[B];
+        js[0] = __builtin_ctzll(todo);
         todo &= todo - 1;
-        const uint32_t* jb = lane_ptr(m.base, j);
-        const uint32_t p = __builtin_amdgcn_readlane(m.pos, j);
 #pragma unroll
-        for (int c = 0; c < W / WAVE; c++) {
-            uint32_t idx = p + (uint32_t)(c * WAVE + lane);
-            if (idx >= (uint32_t)MT_WORDS) idx -= MT_WORDS;
-            const int t = (int)(mt_temper(jb[idx]) & 255u);
-            const uint32_t t1 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x101, 0xF, 0xF, true);  // row_shl:1
-            const uint32_t t2 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x102, 0xF, 0xF, true);  // row_shl:2
-            const uint32_t t3 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x103, 0xF, 0xF, true);  // row_shl:3
-            if ((lane & 3) == 0)
-                *(uint32_t*)(area + j * STRIDE + c * WAVE + lane) = (uint32_t)t | (t1 << 8) | (t2 << 16) | (t3 << 24);
+        for (int b = 1; b < B; b++) {
+            js[b] = todo ? __builtin_ctzll(todo) : js[0];
+            todo &= todo - 1;
         }
-        if (lane == j) {
-            m.sp = p;
-            m.sn = W;
+        uint32_t ps[B], v[B][C];
+#pragma unroll
+        for (int b = 0; b < B; b++) {
+            const uint32_t* jb = lane_ptr(m.base, js[b]);
+            ps[b] = __builtin_amdgcn_readlane(m.pos, js[b]);
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                uint32_t idx = ps[b] + (uint32_t)(c * WAVE + lane);
+                if (idx >= (uint32_t)MT_WORDS) idx -= MT_WORDS;
+                v[b][c] = jb[idx];
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < B; b++) {
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                const int t = (int)(mt_temper(v[b][c]) & 255u);
+                const uint32_t t1 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x101, 0xF, 0xF, true);  // row_shl:1
+                const uint32_t t2 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x102, 0xF, 0xF, true);  // row_shl:2
+                const uint32_t t3 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x103, 0xF, 0xF, true);  // row_shl:3
+                if ((lane & 3) == 0)
+                    *(uint32_t*)(area + js[b] * STRIDE + c * WAVE + lane) =
+                        (uint32_t)t | (t1 << 8) | (t2 << 16) | (t3 << 24);
+            }
+            if (lane == js[b]) {
+                m.sp = ps[b];
+                m.sn = W;
+            }
         }
     }
     wave_sync_lds();

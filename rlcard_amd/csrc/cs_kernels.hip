@@ -153,7 +153,7 @@ template <class G, class M>
 __device__ __forceinline__ void restage(M& m, uint8_t* area, int lane)
 {
     if constexpr (G::STAGE_MODE == STAGE_REGS) m.template restage_regs<G::STAGE_R>();
-    else if constexpr (G::STAGE_MODE == STAGE_LDS) mt_restage_wave<G::STAGE_W, G::STAGE_R>(m, area, lane);
+    else if constexpr (G::STAGE_MODE == STAGE_LDS) mt_restage_wave<G::STAGE_W, G::STAGE_R, G::RESTAGE_B>(m, area, lane);
 }
 template <class G>
 struct Scratch {

@@ -28,6 +28,7 @@ struct Leduc {
     static constexpr bool RAW_OBS = false;
     static constexpr int SCRATCH_WORDS = 0;
     static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 64, STAGE_R = CS_LEDUC_STAGE_R;  // MT staging (see MtLaneT)
+    static constexpr int RESTAGE_B = 4;  // lanes restaged per pass (loads in flight), measured: 4 > 8 > 1
     __device__ __forceinline__ void bind(uint32_t*, const GameParams&) {}
     enum { CALL = 0, RAISE = 1, FOLD = 2, CHECK = 3 };
 

@@ -102,6 +102,7 @@ struct Limit {
     static constexpr bool RAW_OBS = false;
     static constexpr int SCRATCH_WORDS = 0;
     static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_R = 100;  // MT staging (see MtLaneT)
+    static constexpr int RESTAGE_B = 8;  // lanes restaged per pass (loads in flight), measured: 8 > 4 > 1
     __device__ __forceinline__ void bind(uint32_t*, const GameParams&) {}
     enum { CALL = 0, RAISE = 1, FOLD = 2, CHECK = 3 };
 

@@ -16,6 +16,6 @@ for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
            "TD_BUSY_sum TD_TD_BUSY_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCC_EA0_WRREQ_sum TCC_EA0_RDREQ_sum" \
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $O/p$i -o p -- python3 tools/ab_rollout.py $GAME $N $T 0 > $O/run$i.log 2>&1 || echo "pass $i failed" >> $O/errors.log
+  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $O/p$i -o p -- python3 tools/ab_rollout.py $GAME $N $T 0 > $O/run$i.log 2>&1 || { echo "pass $i failed" >> $O/errors.log; exit 20; }
 done
 python3 tools/pmc_summary.py $O > $O/summary.txt 2>&1
