@@ -29,7 +29,8 @@ namespace ddz {
 constexpr int BLOCK = 256;
 constexpr int WPB = BLOCK / WAVE;
 constexpr int MASK_PAD = 4;                       // zero dwords on both sides of the mask image
-constexpr int MASK_WORDS = MASK_PAD + 860 + MASK_PAD;
+constexpr int KTH_LANES = 54, KTH_WORDS = 16;     // kth_legal: lane l scans mask dwords [16 l, 16 l + 16)
+constexpr int MASK_WORDS = MASK_PAD + KTH_LANES * KTH_WORDS + MASK_PAD;
 constexpr int NSEG = 20;                          // 54-bit obs blocks (16 used) + zero tail
 constexpr int BV_WORDS = 32;                      // obs bits (912 + 16 front pad) as dwords
 
@@ -38,8 +39,21 @@ struct WaveLds {
     uint64_t segv[NSEG];         // obs 54-bit blocks
     uint32_t bv[BV_WORDS];       // obs bit x at bit 16 + x
     uint16_t pre[MAX_GROUPS + 8];
-    uint16_t list[ND + 1];       // mask dwords that survived pass b, ascending
 };
+
+// the group table and the per-dword group ranges, copied once per block (read by every step's scan)
+struct TabLds {
+    uint4 grp[MAX_GROUPS];
+    uint32_t drange[ND + 1];
+};
+
+__device__ __forceinline__ void load_tab(TabLds& T, const Tab& tb)
+{
+    const uint4* g = (const uint4*)tb.grp;
+    for (int i = threadIdx.x; i < tb.ng; i += blockDim.x) T.grp[i] = g[i];
+    for (int i = threadIdx.x; i < ND; i += blockDim.x) T.drange[i] = tb.drange[i];
+    __syncthreads();
+}
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, k); }
 __device__ __forceinline__ uint64_t rl64(uint64_t v, int k)
@@ -81,6 +95,7 @@ struct Env {
     // hw4 is unused). Separate scalars, not an array: a lane-indexed pick from an array sends it to scratch.
     uint32_t hw0, hw1, hw2, hw3, hw4;
     uint32_t ntrace, greater, gplay, cur, winner;
+    uint32_t ggrp;              // (type, weight) group of gplay (kept in the spare high half of state word 16)
 
     __device__ __forceinline__ uint32_t hist(uint32_t k) const   // k may differ per lane
     {
@@ -113,7 +128,9 @@ struct Env {
         hw1 = rl(w, W_HIST + 1);
         hw2 = rl(w, W_HIST + 2);
         hw3 = rl(w, W_HIST + 3);
-        hw4 = rl(w, W_HIST + 4) | (NO_ACTION << 16);
+        const uint32_t w16 = rl(w, W_HIST + 4);
+        hw4 = w16 | (NO_ACTION << 16);
+        ggrp = w16 >> 16;
         ntrace = rl(w, W_NTRACE);
         const uint32_t g = rl(w, W_GREATER), c = rl(w, W_CUR);
         greater = g & 0xFFFFu;
@@ -129,7 +146,7 @@ struct Env {
             o[1] = make_uint4((uint32_t)h2, (uint32_t)(h2 >> 32), (uint32_t)q0, (uint32_t)(q0 >> 32));
             o[2] = make_uint4((uint32_t)q1, (uint32_t)(q1 >> 32), (uint32_t)q2, (uint32_t)(q2 >> 32));
             o[3] = make_uint4(hw0, hw1, hw2, hw3);
-            o[4] = make_uint4(hw4, ntrace, greater | (gplay << 16), cur | (winner << 8));
+            o[4] = make_uint4((hw4 & 0xFFFFu) | (ggrp << 16), ntrace, greater | (gplay << 16), cur | (winner << 8));
         }
     }
 
@@ -145,6 +162,7 @@ struct Env {
         ntrace++;
         if (a != (uint32_t)PASS) {
             const uint64_t c = tb.cnt[a];
+            ggrp = tb.gid[a];
             const uint64_t c0 = keep64(p == 0, c), c1 = keep64(p == 1, c), c2 = keep64(p == 2, c);
             h0 -= c0; h1 -= c1; h2 -= c2;
             q0 += c0; q1 += c1; q2 += c2;
@@ -167,7 +185,7 @@ struct Cand {
         return (x - c_lo < c_len) | (x - b_lo < b_len) | (x - r_lo < r_len);
     }
 };
-__device__ __forceinline__ Cand cand_of(const Env& e, const Tab& tb)
+__device__ __forceinline__ Cand cand_of(const Env& e, const Tab& tb, const TabLds& T)
 {
     Cand c;
     c.leading = e.greater == NONE || e.greater == e.cur;   // player.py:60-86 available_actions
@@ -175,8 +193,8 @@ __device__ __forceinline__ Cand cand_of(const Env& e, const Tab& tb)
         c.c_lo = 0; c.c_len = PASS; c.b_lo = 0; c.b_len = 0; c.r_lo = 0; c.r_len = 0;
         return c;
     }
-    const uint32_t g = tb.gid[e.gplay];
-    const uint32_t z = tb.grp[g * 4 + 2], y = tb.grp[g * 4 + 3];
+    const uint4 q = T.grp[e.ggrp];
+    const uint32_t z = q.z, y = q.w;
     const uint32_t gend = z >> 16, tend = y & 0xFFFFu, type = (y >> 16) & 0xFFu;
     if (type == (uint32_t)TYPE_ROCKET) {
         c.c_lo = 0; c.c_len = 0; c.b_lo = 0; c.b_len = 0; c.r_lo = 0; c.r_len = 0;
@@ -276,6 +294,7 @@ __device__ __forceinline__ void deal(Env& e, WaveMt& m, int lane)
     e.h0 = h0; e.h1 = h1; e.h2 = h2;
     e.q0 = e.q1 = e.q2 = 0;
     e.hw0 = e.hw1 = e.hw2 = e.hw3 = e.hw4 = 0xFFFFFFFFu;
+    e.ggrp = 0;
     e.ntrace = 0;
     e.greater = NONE;
     e.gplay = 0;
@@ -286,56 +305,61 @@ __device__ __forceinline__ void deal(Env& e, WaveMt& m, int lane)
 // ---- legal mask ------------------------------------------------------------------------------------------------
 struct Legal {
     uint32_t total;   // legal combos (pass not included)
-    uint32_t nl;      // surviving dwords in L.list
 };
 
 __device__ __forceinline__ void zero_mask(WaveLds& L, int lane)
 {
     uint4* z = (uint4*)L.mask;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
+    for (int j = 0; j < (MASK_WORDS / 4 + WAVE - 1) / WAVE; j++) {
         const int q = j * WAVE + lane;
         if (q < MASK_WORDS / 4) z[q] = make_uint4(0, 0, 0, 0);
     }
 }
 
-__device__ __forceinline__ void test_pair(int da, int db, uint64_t h, const Cand& c, const Tab& tb, WaveLds& L,
-                                          int lane, Legal& r)
+// pass c for up to PAIRS x 2 surviving dwords: lanes 0..31 take the even slot of a pair, 32..63 the odd one; all
+// the id loads are issued before the first test (slots < 0 are empty)
+constexpr int PAIRS = 4;
+__device__ __forceinline__ void test_dwords(const int (&ds)[2 * PAIRS], uint64_t h, const Cand& c, const Tab& tb,
+                                            WaveLds& L, int lane, Legal& r)
 {
-    const int d = lane < 32 ? da : db;
-    const uint32_t id = (uint32_t)d * 32u + (uint32_t)(lane & 31);
-    bool ok = false;
-    if (d >= 0 && id < (uint32_t)PASS) ok = contains(h, tb.cnt[id]) && c.ok(id);
-    const uint64_t m = __ballot(ok);
-    if (lane == 0) {
-        L.mask[MASK_PAD + da] = (uint32_t)m;
-        L.list[r.nl] = (uint16_t)da;
-        if (db >= 0) {
-            L.mask[MASK_PAD + db] = (uint32_t)(m >> 32);
-            L.list[r.nl + 1] = (uint16_t)db;
-        }
+    uint64_t cnt[PAIRS];
+    uint32_t id[PAIRS];
+    bool live[PAIRS];
+#pragma unroll
+    for (int q = 0; q < PAIRS; q++) {
+        const int d = lane < 32 ? ds[2 * q] : ds[2 * q + 1];
+        id[q] = (uint32_t)d * 32u + (uint32_t)(lane & 31);
+        live[q] = d >= 0 && id[q] < (uint32_t)PASS;
+        cnt[q] = live[q] ? tb.cnt[id[q]] : ~0ull;
     }
-    r.nl += db >= 0 ? 2u : 1u;
-    r.total += (uint32_t)__popcll(m);
+#pragma unroll
+    for (int q = 0; q < PAIRS; q++) {
+        const uint64_t m = __ballot(live[q] && contains(h, cnt[q]) && c.ok(id[q]));
+        if (lane == 0) {
+            if (ds[2 * q] >= 0) L.mask[MASK_PAD + ds[2 * q]] = (uint32_t)m;
+            if (ds[2 * q + 1] >= 0) L.mask[MASK_PAD + ds[2 * q + 1]] = (uint32_t)(m >> 32);
+        }
+        r.total += (uint32_t)__popcll(m);
+    }
 }
 
 // mask image must be zero on entry
-__device__ __forceinline__ Legal build_legal(const Env& e, const Cand& c, const Tab& tb, WaveLds& L, int lane)
+__device__ __forceinline__ Legal build_legal(const Env& e, const Cand& c, const Tab& tb, const TabLds& T, WaveLds& L,
+                                             int lane)
 {
     Legal r;
     r.total = 0;
-    r.nl = 0;
     if (e.over()) return r;                                        // game.py:110-128: no actions once over
     const uint64_t h = e.hand(e.cur);
     // a. groups
     uint32_t base = 0;
-    const uint4* grp = (const uint4*)tb.grp;
 #pragma unroll
     for (int k = 0; k < MAX_GROUPS / WAVE; k++) {
         const int g = k * WAVE + lane;
         bool pass = false;
         if (g < tb.ng) {
-            const uint4 q = grp[g];
+            const uint4 q = T.grp[g];
             pass = contains(h, (uint64_t)q.x | ((uint64_t)q.y << 32)) && c.ok(q.z & 0xFFFFu);
         }
         const uint64_t b = __ballot(pass);
@@ -344,57 +368,64 @@ __device__ __forceinline__ Legal build_legal(const Env& e, const Cand& c, const 
     }
     if (base == 0) return r;
     wave_sync_lds();
-    // b. dwords that any passing group overlaps, c. their ids, two dwords per wave pass
-    int pend = -1;
+    // b. dwords that any passing group overlaps; c. their ids, up to 2 x PAIRS dwords per batch
     for (int k = 0; k < (ND + WAVE - 1) / WAVE; k++) {
         const int d = k * WAVE + lane;
         bool pass = false;
         if (d < ND) {
-            const uint32_t dr = tb.drange[d];
+            const uint32_t dr = T.drange[d];
             pass = L.pre[(dr >> 16) + 1] > L.pre[dr & 0xFFFFu];
         }
         uint64_t bits = __ballot(pass);
         while (bits) {
-            const int dd = k * WAVE + __builtin_ctzll(bits);
-            bits &= bits - 1;
-            if (pend < 0) {
-                pend = dd;
-            } else {
-                test_pair(pend, dd, h, c, tb, L, lane, r);
-                pend = -1;
+            int ds[2 * PAIRS];
+#pragma unroll
+            for (int j = 0; j < 2 * PAIRS; j++) {
+                ds[j] = bits ? k * WAVE + __builtin_ctzll(bits) : -1;
+                bits &= bits - 1;
             }
+            test_dwords(ds, h, c, tb, L, lane, r);
         }
     }
-    if (pend >= 0) test_pair(pend, -1, h, c, tb, L, lane, r);
     return r;
 }
 
-// the k-th legal id in ascending order (k < total + !leading; pass is the largest id)
+// the k-th legal id in ascending order (k < total + !leading; pass is the largest id): lane l counts the legal bits
+// of mask dwords [16 l, 16 l + 16), a wave prefix scan finds the lane, 16 lanes then find the dword
 __device__ __forceinline__ uint32_t kth_legal(uint32_t k, const Legal& r, const WaveLds& L, int lane)
 {
     if (k >= r.total) return (uint32_t)PASS;
-    for (uint32_t b0 = 0; b0 < r.nl; b0 += WAVE) {
-        const uint32_t i = b0 + (uint32_t)lane;
-        const uint32_t d = i < r.nl ? L.list[i] : 0u;
-        const uint32_t w = i < r.nl ? L.mask[MASK_PAD + d] : 0u;
-        const uint32_t pc = (uint32_t)__popc(w);
-        uint32_t inc = pc;
+    uint32_t pc = 0;
+    if (lane < KTH_LANES) {
+        const uint4* w = (const uint4*)(L.mask + MASK_PAD) + lane * (KTH_WORDS / 4);
 #pragma unroll
-        for (int o = 1; o < WAVE; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
-            if (lane >= o) inc += y;
+        for (int j = 0; j < KTH_WORDS / 4; j++) {
+            const uint4 x = w[j];
+            pc += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
         }
-        const uint32_t tot = rl(inc, WAVE - 1);
-        if (k < tot) {
-            const int j = __builtin_ctzll(__ballot(inc > k));
-            uint32_t word = rl(w, j);
-            uint32_t kk = k - (rl(inc, j) - rl(pc, j));
-            while (kk--) word &= word - 1;
-            return rl(d, j) * 32u + (uint32_t)__builtin_ctz(word);
-        }
-        k -= tot;
     }
-    return (uint32_t)PASS;   // unreachable
+    uint32_t inc = pc;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+        if (lane >= o) inc += y;
+    }
+    const int j = __builtin_ctzll(__ballot(inc > k));
+    k -= rl(inc, j) - rl(pc, j);
+    // second level: the 16 dwords of lane j
+    const uint32_t w = lane < KTH_WORDS ? L.mask[MASK_PAD + j * KTH_WORDS + lane] : 0u;
+    const uint32_t p2 = (uint32_t)__popc(w);
+    uint32_t inc2 = p2;
+#pragma unroll
+    for (int o = 1; o < KTH_WORDS; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc2, o);
+        if (lane >= o) inc2 += y;
+    }
+    const int q = __builtin_ctzll(__ballot(lane < KTH_WORDS && inc2 > k));
+    uint32_t word = rl(w, q);
+    uint32_t kk = k - (rl(inc2, q) - rl(p2, q));
+    while (kk--) word &= word - 1;
+    return (uint32_t)(j * KTH_WORDS + q) * 32u + (uint32_t)__builtin_ctz(word);
 }
 
 // ---- obs -------------------------------------------------------------------------------------------------------
@@ -547,13 +578,13 @@ __device__ __forceinline__ WaveMt wave_mt(uint32_t* mt, const uint32_t* ctl, int
 }
 
 // obs / legal / player / done of the current state, for `self` (observe) or the current player
-__device__ __forceinline__ void emit_state(const Env& e, uint32_t self, const Tab& tb, WaveLds& L, int lane,
-                                           int64_t row, const cs_step_out& out)
+__device__ __forceinline__ void emit_state(const Env& e, uint32_t self, const Tab& tb, const TabLds& T, WaveLds& L,
+                                           int lane, int64_t row, const cs_step_out& out)
 {
     zero_mask(L, lane);
     wave_sync_lds();
-    const Cand cd = cand_of(e, tb);
-    build_legal(e, cd, tb, L, lane);
+    const Cand cd = cand_of(e, tb, T);
+    build_legal(e, cd, tb, T, L, lane);
     if (!e.over() && !cd.leading && lane == 0) L.mask[MASK_PAD + PASS / 32] |= 1u << (PASS & 31);
     build_obs(e, self, tb, L, lane);
     wave_sync_lds();
@@ -576,13 +607,15 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, ui
                                                   cs_step_out out, Tab tb)
 {
     __shared__ WaveLds lds[WPB];
+    __shared__ TabLds tl;
+    load_tab(tl, tb);                 // every thread of the block, before any wave leaves
     const Ctx c = ctx_of(n);
     if (!c.valid) return;
     WaveLds& L = lds[c.wid];
     Env e;
     WaveMt m = wave_mt(mt, ctl, c.env);
     deal(e, m, c.lane);
-    emit_state(e, e.cur, tb, L, c.lane, c.env, out);
+    emit_state(e, e.cur, tb, tl, L, c.lane, c.env, out);
     if (c.lane == 0 && out.reward) {
         float* r = (float*)out.reward + c.env * P;
         r[0] = r[1] = r[2] = 0.f;
@@ -595,6 +628,8 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uin
                                                  const int32_t* actions, cs_step_out out, Tab tb)
 {
     __shared__ WaveLds lds[WPB];
+    __shared__ TabLds tl;
+    load_tab(tl, tb);                 // every thread of the block, before any wave leaves
     const Ctx c = ctx_of(n);
     if (!c.valid) return;
     WaveLds& L = lds[c.wid];
@@ -606,12 +641,12 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uin
     if (e.over()) {
         deal(e, m, c.lane);
     } else {
-        const Cand cd = cand_of(e, tb);
+        const Cand cd = cand_of(e, tb, tl);
         e.apply(decode_action(actions[c.env], e, cd, tb), tb);
         done = e.over();
         if (done) payoffs(e, r);
     }
-    emit_state(e, e.cur, tb, L, c.lane, c.env, out);
+    emit_state(e, e.cur, tb, tl, L, c.lane, c.env, out);
     if (c.lane == 0) {
         if (out.reward) {
             float* o = (float*)out.reward + c.env * P;
@@ -626,11 +661,13 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uin
 __global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n, int player, cs_step_out out, Tab tb)
 {
     __shared__ WaveLds lds[WPB];
+    __shared__ TabLds tl;
+    load_tab(tl, tb);                 // every thread of the block, before any wave leaves
     const Ctx c = ctx_of(n);
     if (!c.valid) return;
     Env e;
     e.load(st, c.env, c.lane);
-    emit_state(e, (uint32_t)player, tb, lds[c.wid], c.lane, c.env, out);
+    emit_state(e, (uint32_t)player, tb, tl, lds[c.wid], c.lane, c.env, out);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n, int T,
@@ -638,6 +675,8 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, 
                                                     Tab tb)
 {
     __shared__ WaveLds lds[WPB];
+    __shared__ TabLds tl;
+    load_tab(tl, tb);                 // every thread of the block, before any wave leaves
     const Ctx c = ctx_of(n);
     if (!c.valid) return;
     WaveLds& L = lds[c.wid];
@@ -651,8 +690,8 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, 
         const int64_t row = (int64_t)t * n + c.env;
         zero_mask(L, lane);
         wave_sync_lds();
-        const Cand cd = cand_of(e, tb);
-        const Legal lg = build_legal(e, cd, tb, L, lane);
+        const Cand cd = cand_of(e, tb, tl);
+        const Legal lg = build_legal(e, cd, tb, tl, L, lane);
         build_obs(e, e.cur, tb, L, lane);
         wave_sync_lds();
         const uint32_t count = lg.total + (cd.leading ? 0u : 1u);
