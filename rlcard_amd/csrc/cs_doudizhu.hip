@@ -96,6 +96,8 @@ struct Env {
     uint32_t hw0, hw1, hw2, hw3, hw4;
     uint32_t ntrace, greater, gplay, cur, winner;
     uint32_t ggrp;              // (type, weight) group of gplay (kept in the spare high half of state word 16)
+    uint64_t hcnt;              // PER LANE: lane s = 3..11 holds the packed counts of hist(s - 3) (0: pass / none),
+                                // shifted down one lane per action, so observations never reload the action table
 
     __device__ __forceinline__ uint32_t hist(uint32_t k) const   // k may differ per lane
     {
@@ -115,7 +117,7 @@ struct Env {
     }
     __device__ __forceinline__ bool over() const { return winner != NONE; }
 
-    __device__ __forceinline__ void load(const uint32_t* st, int64_t env, int lane)
+    __device__ __forceinline__ void load(const uint32_t* st, int64_t env, int lane, const Tab& tb)
     {
         const uint32_t w = lane < WORDS ? st[env * WORDS + lane] : 0u;
         h0 = (uint64_t)rl(w, 0) | ((uint64_t)rl(w, 1) << 32);
@@ -131,6 +133,8 @@ struct Env {
         const uint32_t w16 = rl(w, W_HIST + 4);
         hw4 = w16 | (NO_ACTION << 16);
         ggrp = w16 >> 16;
+        const uint32_t id = lane >= 3 && lane <= 11 ? hist((uint32_t)(lane - 3)) : NO_ACTION;
+        hcnt = id < (uint32_t)PASS ? tb.cnt[id] : 0ull;
         ntrace = rl(w, W_NTRACE);
         const uint32_t g = rl(w, W_GREATER), c = rl(w, W_CUR);
         greater = g & 0xFFFFu;
@@ -151,9 +155,13 @@ struct Env {
     }
 
     // Player.play + Round.proceed_round + Game.step (player.py:88-108, round.py:54-79, game.py:55-81)
-    __device__ __forceinline__ void apply(uint32_t a, const Tab& tb)
+    __device__ __forceinline__ void apply(uint32_t a, const Tab& tb, int lane)
     {
         const uint32_t p = cur;
+        const uint64_t c = a != (uint32_t)PASS ? tb.cnt[a] : 0ull;
+        const uint64_t down = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)hcnt, 1) |
+                              ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(hcnt >> 32), 1) << 32);
+        hcnt = lane == 11 ? c : (lane >= 3 && lane < 11 ? down : 0ull);
         hw0 = (hw0 >> 16) | (hw1 << 16);
         hw1 = (hw1 >> 16) | (hw2 << 16);
         hw2 = (hw2 >> 16) | (hw3 << 16);
@@ -161,7 +169,6 @@ struct Env {
         hw4 = a | (NO_ACTION << 16);
         ntrace++;
         if (a != (uint32_t)PASS) {
-            const uint64_t c = tb.cnt[a];
             ggrp = tb.gid[a];
             const uint64_t c0 = keep64(p == 0, c), c1 = keep64(p == 1, c), c2 = keep64(p == 2, c);
             h0 -= c0; h1 -= c1; h2 -= c2;
@@ -295,6 +302,7 @@ __device__ __forceinline__ void deal(Env& e, WaveMt& m, int lane)
     e.q0 = e.q1 = e.q2 = 0;
     e.hw0 = e.hw1 = e.hw2 = e.hw3 = e.hw4 = 0xFFFFFFFFu;
     e.ggrp = 0;
+    e.hcnt = 0;
     e.ntrace = 0;
     e.greater = NONE;
     e.gplay = 0;
@@ -368,7 +376,11 @@ __device__ __forceinline__ Legal build_legal(const Env& e, const Cand& c, const 
     }
     if (base == 0) return r;
     wave_sync_lds();
-    // b. dwords that any passing group overlaps; c. their ids, up to 2 x PAIRS dwords per batch
+    // b. dwords that any passing group overlaps; c. their ids, 2 x PAIRS dwords per batch (collected across chunks)
+    int ds[2 * PAIRS];
+#pragma unroll
+    for (int j = 0; j < 2 * PAIRS; j++) ds[j] = -1;
+    int nf = 0;
     for (int k = 0; k < (ND + WAVE - 1) / WAVE; k++) {
         const int d = k * WAVE + lane;
         bool pass = false;
@@ -378,15 +390,19 @@ __device__ __forceinline__ Legal build_legal(const Env& e, const Cand& c, const 
         }
         uint64_t bits = __ballot(pass);
         while (bits) {
-            int ds[2 * PAIRS];
 #pragma unroll
-            for (int j = 0; j < 2 * PAIRS; j++) {
-                ds[j] = bits ? k * WAVE + __builtin_ctzll(bits) : -1;
-                bits &= bits - 1;
+            for (int j = 0; j < 2 * PAIRS - 1; j++) ds[j] = ds[j + 1];
+            ds[2 * PAIRS - 1] = k * WAVE + __builtin_ctzll(bits);
+            bits &= bits - 1;
+            if (++nf == 2 * PAIRS) {
+                test_dwords(ds, h, c, tb, L, lane, r);
+#pragma unroll
+                for (int j = 0; j < 2 * PAIRS; j++) ds[j] = -1;
+                nf = 0;
             }
-            test_dwords(ds, h, c, tb, L, lane, r);
         }
     }
+    if (nf) test_dwords(ds, h, c, tb, L, lane, r);
     return r;
 }
 
@@ -434,32 +450,27 @@ __device__ __forceinline__ uint32_t kth_legal(uint32_t k, const Legal& r, const 
 //   landlord: 12 / 13 cards played by players 2 / 1, one-hots of their hand sizes at 756 / 773 (17 wide);
 //   peasant:  12 / 13 cards played by the landlord / teammate, 14 / 15 their last actions, one-hots of their hand
 //             sizes at 864 (20 wide) / 884 (17 wide).
-__device__ __forceinline__ void build_obs(const Env& e, uint32_t self, const Tab& tb, WaveLds& L, int lane)
+__device__ __forceinline__ void build_obs(const Env& e, uint32_t self, WaveLds& L, int lane)
 {
     const uint32_t nt = e.ntrace;
-    const uint32_t h8 = e.hw4 & 0xFFFFu, h7 = e.hw3 >> 16, h6 = e.hw3 & 0xFFFFu;
-    uint32_t last = h8;
-    if (last == (uint32_t)PASS) last = h7;
+    const uint32_t h8 = e.hw4 & 0xFFFFu;
     const uint32_t mate = 3u - self;
-    uint32_t ll = NO_ACTION, lt = NO_ACTION;
+    const uint64_t last_c = rl64(e.hcnt, h8 == (uint32_t)PASS ? 10 : 11);   // last non-pass action (h8, else h7)
+    uint64_t ll_c = 0, lt_c = 0;                                               // landlord's / teammate's last action
     if (self != 0) {
-        if (nt >= 1u) ll = (nt - 1u) % 3u == 0u ? h8 : ((nt - 1u) % 3u == 1u ? h7 : h6);
-        if (nt > mate) {
-            const uint32_t d = (nt - 1u - mate) % 3u;
-            lt = d == 0u ? h8 : (d == 1u ? h7 : h6);
-        }
+        if (nt >= 1u) ll_c = rl64(e.hcnt, 11 - (int)((nt - 1u) % 3u));
+        if (nt > mate) lt_c = rl64(e.hcnt, 11 - (int)((nt - 1u - mate) % 3u));
     }
     const int s = lane;
-    uint32_t id = NO_ACTION;
     uint64_t direct = 0;
     if (s == 0) direct = e.hand(self);
     else if (s == 1) direct = e.hand(self == 0 ? 1u : 0u) + e.hand(self == 2 ? 1u : 2u);
-    else if (s == 2) id = last;
-    else if (s <= 11) id = e.hist((uint32_t)(s - 3)); else if (s == 12) direct = self == 0 ? e.q2 : e.q0;
+    else if (s == 2) direct = last_c;
+    else if (s <= 11) direct = e.hcnt;
+    else if (s == 12) direct = self == 0 ? e.q2 : e.q0;
     else if (s == 13) direct = self == 0 ? e.q1 : e.played(mate);
-    else if (s == 14 && self != 0) id = ll;
-    else if (s == 15 && self != 0) id = lt;
-    if (id < (uint32_t)PASS) direct = tb.cnt[id];
+    else if (s == 14) direct = ll_c;
+    else if (s == 15) direct = lt_c;
     if (s < NSEG) L.segv[s] = cards_bits(direct);
     uint32_t p1, p2;
     if (self == 0) {
@@ -586,7 +597,7 @@ __device__ __forceinline__ void emit_state(const Env& e, uint32_t self, const Ta
     const Cand cd = cand_of(e, tb, T);
     build_legal(e, cd, tb, T, L, lane);
     if (!e.over() && !cd.leading && lane == 0) L.mask[MASK_PAD + PASS / 32] |= 1u << (PASS & 31);
-    build_obs(e, self, tb, L, lane);
+    build_obs(e, self, L, lane);
     wave_sync_lds();
     if (out.obs) write_obs_row(L, (uint8_t*)out.obs + row * OBS, lane);
     if (out.legal) write_legal_row(L, (uint8_t*)out.legal + row * LB, lane);
@@ -634,7 +645,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uin
     if (!c.valid) return;
     WaveLds& L = lds[c.wid];
     Env e;
-    e.load(st, c.env, c.lane);
+    e.load(st, c.env, c.lane, tb);
     WaveMt m = wave_mt(mt, ctl, c.env);
     float r[3] = {0.f, 0.f, 0.f};
     bool done = false;
@@ -642,7 +653,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uin
         deal(e, m, c.lane);
     } else {
         const Cand cd = cand_of(e, tb, tl);
-        e.apply(decode_action(actions[c.env], e, cd, tb), tb);
+        e.apply(decode_action(actions[c.env], e, cd, tb), tb, c.lane);
         done = e.over();
         if (done) payoffs(e, r);
     }
@@ -666,7 +677,7 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n
     const Ctx c = ctx_of(n);
     if (!c.valid) return;
     Env e;
-    e.load(st, c.env, c.lane);
+    e.load(st, c.env, c.lane, tb);
     emit_state(e, (uint32_t)player, tb, tl, lds[c.wid], c.lane, c.env, out);
 }
 
@@ -682,7 +693,7 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, 
     WaveLds& L = lds[c.wid];
     const int lane = c.lane;
     Env e;
-    e.load(st, c.env, lane);
+    e.load(st, c.env, lane, tb);
     WaveMt m = wave_mt(mt, ctl, c.env);
     if (e.over()) deal(e, m, lane);
     const uint64_t genv = env_base + (uint64_t)c.env;
@@ -692,7 +703,7 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, 
         wave_sync_lds();
         const Cand cd = cand_of(e, tb, tl);
         const Legal lg = build_legal(e, cd, tb, tl, L, lane);
-        build_obs(e, e.cur, tb, L, lane);
+        build_obs(e, e.cur, L, lane);
         wave_sync_lds();
         const uint32_t count = lg.total + (cd.leading ? 0u : 1u);
         const uint32_t rr = philox_u32(seed, genv, t0 + (uint64_t)t);
@@ -702,7 +713,7 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, 
         write_obs_row(L, (uint8_t*)out.obs + row * OBS, lane);
         write_legal_row(L, (uint8_t*)out.legal + row * LB, lane);
         const uint32_t p = e.cur;
-        e.apply(a, tb);
+        e.apply(a, tb, lane);
         const bool done = e.over();
         if (lane == 0) {
             ((uint8_t*)out.player)[row] = (uint8_t)p;
