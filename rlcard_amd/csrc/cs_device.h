@@ -199,6 +199,45 @@ struct MtLaneT {
         return v;
     }
 
+    // pos += n (n < 624 staged words), with advance()'s block bookkeeping
+    __device__ __forceinline__ void advance_by(uint32_t n)
+    {
+        uint32_t np = pos + n;
+        const bool crossed = pos < (uint32_t)MT_N ? np >= (uint32_t)MT_N : np >= (uint32_t)MT_WORDS;
+        if (np >= (uint32_t)MT_WORDS) np -= MT_WORDS;
+        if (crossed) {
+            if (stale) mt_twist_serial(base + (np < (uint32_t)MT_N ? MT_N : 0), base + (np < (uint32_t)MT_N ? 0 : MT_N));
+            stale = 1;
+        }
+        pos = np;
+    }
+
+    // random_interval(i) for i = hi, hi - 1, ..., 1 with every result discarded (shuffle positions nobody is dealt
+    // from): acceptance only decides how many words are consumed, so the staged bytes are scanned branch-free, four
+    // per LDS read. A lane that runs out of staged bytes finishes through interval() (global loads).
+    __device__ __forceinline__ void skip_intervals(uint32_t hi)
+    {
+        uint32_t i = hi;
+        if constexpr (MODE == STAGE_LDS) {
+            const uint32_t k0 = staged_offset();
+            uint32_t k = k0;
+            while (i != 0 && k < sn) {
+                const uint32_t sh = k & 3u;
+                const uint32_t w = *(const uint32_t*)(stg + (k - sh)) >> (8 * sh);
+#pragma unroll
+                for (uint32_t t = 0; t < 4; t++) {
+                    if (t < 4 - sh && i != 0 && k < sn) {
+                        const uint32_t u = (w >> (8 * t)) & (0xFFFFFFFFu >> __builtin_clz(i));
+                        i -= u <= i ? 1u : 0u;
+                        k++;
+                    }
+                }
+            }
+            advance_by(k - k0);
+        }
+        for (; i >= 1; i--) (void)interval(i);
+    }
+
     // STAGE_REGS restage (per lane, no cross-lane work): a lane with fewer than R staged draws left loads the
     // 16-word chunk starting at pos & ~3 (four 16-B loads, wrapping at the end of the 1248-word ring), tempers it and
     // keeps the low bytes. All needy lanes load in the same wave instructions.
@@ -294,12 +333,14 @@ __device__ __forceinline__ void mt_refill_wave(M& m, int lane)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// STAGE_LDS rows: W bytes per lane (W multiple of 64), row stride W + 16 (16-B aligned rows for the b128 copies that
-// persist them in HBM between launches; consecutive rows land on shifted banks).
+// STAGE_LDS rows: W bytes per lane (W multiple of 64). Row stride W + 16 (16-B copies persist the rows in HBM between
+// launches) or, for W >= 128, W + 8 with 8-B copies: Limit's occupancy is LDS-bound and stride 136 fits 3 blocks per
+// CU where 144 fit 2 (measured: Limit 1.405 -> 1.339 ms/launch; Leduc's W = 64 is 2 % faster at stride 80 than 72).
 template <int W>
 struct Stage {
     static_assert(W % WAVE == 0, "LDS staging rows are filled 64 words per wave instruction");
-    static constexpr int STRIDE = W + 16;
+    static constexpr int STRIDE = W >= 128 ? W + 8 : W + 16;
+    static constexpr int CHUNK = STRIDE % 16 == 0 ? 16 : 8;   // bytes per persist copy
     static constexpr int BYTES = WAVE * STRIDE;
 };
 
@@ -365,20 +406,25 @@ __device__ __forceinline__ void mt_restage_wave(MtLaneT<STAGE_LDS>& m, uint8_t* 
     wave_sync_lds();
 }
 
-// Persist / restore a wave's staging rows (W bytes per env, HBM row-major [env][W]) with coalesced 16-B copies, so a
+// Persist / restore a wave's staging rows (W bytes per env, HBM row-major [env][W]) with coalesced 16-B / 8-B copies, so a
 // launch does not restage every lane from scratch. nvalid = envs of this wave.
 template <int W>
 __device__ __forceinline__ void stage_rows_copy(uint8_t* area, uint8_t* hbm_rows, int lane, int nvalid, bool to_lds)
 {
-    constexpr int STRIDE = Stage<W>::STRIDE, CPR = W / 16;   // 16-B chunks per row
+    constexpr int STRIDE = Stage<W>::STRIDE, CH = Stage<W>::CHUNK, CPR = W / CH;   // chunks per row
 #pragma unroll
     for (int i = 0; i < CPR; i++) {
         const int q = i * WAVE + lane, row = q / CPR, col = q - row * CPR;
         if (row < nvalid) {
-            uint4* l = (uint4*)(area + row * STRIDE + col * 16);
-            uint4* g = (uint4*)(hbm_rows + (size_t)q * 16);
-            if (to_lds) *l = *g;
-            else *g = *l;
+            uint8_t* l = area + row * STRIDE + col * CH;
+            uint8_t* g = hbm_rows + (size_t)q * CH;
+            if constexpr (CH == 16) {
+                if (to_lds) *(uint4*)l = *(const uint4*)g;
+                else *(uint4*)g = *(const uint4*)l;
+            } else {
+                if (to_lds) *(uint2*)l = *(const uint2*)g;
+                else *(uint2*)g = *(const uint2*)l;
+            }
         }
     }
     wave_sync_lds();

@@ -156,9 +156,14 @@ __device__ __forceinline__ void restage(M& m, uint8_t* area, int lane)
     else if constexpr (G::STAGE_MODE == STAGE_LDS) mt_restage_wave<G::STAGE_W, G::STAGE_R, G::RESTAGE_B>(m, area, lane);
 }
 template <class G>
-struct Scratch {
-    static constexpr int WORDS = (G::SCRATCH_WORDS > 0 ? G::SCRATCH_WORDS : 1) * WAVE;
+struct Scratch {   // per-lane LDS words of games that keep state in LDS (blackjack); one word per wave otherwise
+    static constexpr int WORDS = G::SCRATCH_WORDS > 0 ? G::SCRATCH_WORDS * WAVE : 1;
 };
+template <class G>
+__device__ __forceinline__ uint32_t* scratch_of(uint32_t* wave_area, int lane)
+{
+    return G::SCRATCH_WORDS > 0 ? wave_area + lane : nullptr;
+}
 #define CS_SMEM(G)                                                  \
     __shared__ uint32_t lds[WAVES_PER_BLOCK][ObsLds<G>::WORDS];     \
     __shared__ uint32_t scr[WAVES_PER_BLOCK][Scratch<G>::WORDS]
@@ -184,7 +189,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed(uint32_t* mt, uint32_t* ctl, uin
         m.base = base;
         m.stale = 1;                                            // block 1 = twist(block 0), refilled below
         G g;
-        g.bind(&scr[threadIdx.x / WAVE][lane], prm);
+        g.bind(scratch_of<G>(scr[threadIdx.x / WAVE], lane), prm);
         g.blank();
         g.store(st, n, env);
     }
@@ -205,7 +210,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, ui
     const LaneCtx c = lane_ctx(n);
     MtLane m = mt_lane(mt, ctl, c);
     G g;
-    g.bind(&scr[c.wid][c.lane], prm);
+    g.bind(scratch_of<G>(scr[c.wid], c.lane), prm);
     g.blank();
     if (c.valid) {
         g.load(st, n, c.env);   // the Game object outlives init_game (limit-holdem's raise history, :98/:101)
@@ -240,7 +245,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uin
     const LaneCtx c = lane_ctx(n);
     MtLane m = mt_lane(mt, ctl, c);
     G g;
-    g.bind(&scr[c.wid][c.lane], prm);
+    g.bind(scratch_of<G>(scr[c.wid], c.lane), prm);
     g.blank();
     float r[G::P];
 #pragma unroll
@@ -278,7 +283,7 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n
     CS_SMEM(G);
     const LaneCtx c = lane_ctx(n);
     G g;
-    g.bind(&scr[c.wid][c.lane], prm);
+    g.bind(scratch_of<G>(scr[c.wid], c.lane), prm);
     g.blank();
     if (c.valid) g.load(st, n, c.env);
     uint32_t bits[G::NB];
@@ -319,7 +324,7 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, 
         }
     }
     G g;
-    g.bind(&scr[c.wid][c.lane], prm);
+    g.bind(scratch_of<G>(scr[c.wid], c.lane), prm);
     g.blank();
     if (c.valid) {
         g.load(st, n, c.env);

@@ -178,7 +178,7 @@ struct Limit {
             J[k] = j;
             V[k] = vi;
         }
-        for (int i = 42; i >= 1; i--) (void)rng.interval((uint32_t)i);
+        rng.skip_intervals(42u);   // deck positions 42..1 are never dealt: only the words they consume matter
         // hole i -> player i%2, card i/2, from deck[51-i] = D[i]
         const int s = (int)rng.interval(1u);
         const int in_0 = s == 0 ? 1 : 2, in_1 = s == 0 ? 2 : 1;
