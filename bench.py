@@ -11,6 +11,7 @@ trajectory shards (timed separately, reported under "gather").
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -84,6 +85,8 @@ def main():
     ap.add_argument('--T', type=int, default=16, help='fused env steps per launch')
     ap.add_argument('--gather', action='store_true', help='also all-gather trajectory shards over RCCL')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-precondition', dest='precondition', action='store_false',
+                    help='time from freshly seeded streams (optimistic: no MT block refills yet)')
     args = ap.parse_args()
 
     import torch
@@ -113,6 +116,13 @@ def main():
 
     stream = torch.cuda.current_stream()
     t_launch = 0
+    # Precondition: every env's MT19937 stream starts at position 0 after seeding, so no env refills a block until
+    # ~624 draws in; run (untimed) until each stream has crossed two blocks on average, so the timed launches see the
+    # steady-state refill rate (measured on Leduc: launches are ~15-25 % slower once the refills start).
+    pre = int(math.ceil(2 * 624 / (GAMES[game]['draws_per_step'] * T))) if args.precondition else 0
+    for w in range(pre):
+        env.rollout(T, policy_seed=5, t0=t_launch * T, out=traj)
+        t_launch += 1
     for w in range(args.warmup):
         env.rollout(T, policy_seed=5, t0=t_launch * T, out=traj)
         t_launch += 1
@@ -175,7 +185,8 @@ def main():
             'scaling': 'weak',
             'vs_baseline': None,
             'dtype': 'int32',
-            'data': 'synthetic: env i seeded 42+i (reference seeding), uniform-random legal policy (Philox)',
+            'data': 'synthetic: env i seeded 42+i (reference seeding), uniform-random legal policy (Philox); '
+                    '%d untimed preconditioning launches (steady-state MT refill rate)' % pre,
             'config': {'workload': '%s, %d envs per GPU, %d fused lockstep steps per launch, auto-reset, full '
                                    'trajectory to HBM' % (game, N, T),
                        'game': game, 'envs_per_gpu': N, 'global_envs': world * N, 'fused_steps': T,

@@ -30,8 +30,10 @@ struct Blackjack {
     static constexpr int NB = 1;               // raw obs dwords
     static constexpr bool RAW_OBS = true;      // observe() returns byte values, not a 0/1 bitmap
     static constexpr int SCRATCH_WORDS = WORDS;
-    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_R = 100;  // MT staging (see MtLaneT)
+    // MT staging (see MtLaneT)
+    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_PAD = 8, STAGE_R = 100;
     static constexpr int RESTAGE_B = 8;  // lanes restaged per pass (loads in flight), measured: 8 > 4 > 1
+    static constexpr int REFILL_K = 2;   // stale blocks twisted per pass (see mt_refill_wave)
     static constexpr int HAND_CAP = 12;
 
     uint32_t* s;   // lane scratch: word i at s[i * WAVE]

@@ -310,22 +310,25 @@ __device__ __forceinline__ void mt_twist_wave_k(const uint32_t* const (&src)[K],
 
 // End-of-step convergence point: the wave refills every stale block of its lanes, two lanes' twists at a time
 // (their loads overlap; an odd last lane is paired with itself: identical writes, harmless). All 64 lanes must call.
-template <class M>
+template <int K = 2, class M>
 __device__ __forceinline__ void mt_refill_wave(M& m, int lane)
 {
     uint64_t need = __ballot(m.stale != 0);
     while (need) {
-        const int j0 = __builtin_ctzll(need);
-        need &= need - 1;
-        const int j1 = need ? __builtin_ctzll(need) : j0;
-        need &= need - 1;
-        uint32_t* b0 = lane_ptr(m.base, j0);
-        uint32_t* b1 = lane_ptr(m.base, j1);
-        const uint32_t c0 = __builtin_amdgcn_readlane(m.pos, j0) < MT_N ? 0 : MT_N;
-        const uint32_t c1 = __builtin_amdgcn_readlane(m.pos, j1) < MT_N ? 0 : MT_N;
-        const uint32_t* const src[2] = {b0 + c0, b1 + c1};
-        uint32_t* const dst[2] = {b0 + (MT_N - c0), b1 + (MT_N - c1)};
-        mt_twist_wave_k<2>(src, dst, lane);
+        const uint32_t* src[K];
+        uint32_t* dst[K];
+        int j0 = -1;
+#pragma unroll
+        for (int s = 0; s < K; s++) {
+            const int j = need ? __builtin_ctzll(need) : j0;
+            need &= need - 1;
+            if (s == 0) j0 = j;
+            uint32_t* b = lane_ptr(m.base, j);
+            const uint32_t c = __builtin_amdgcn_readlane(m.pos, j) < MT_N ? 0 : MT_N;
+            src[s] = b + c;
+            dst[s] = b + (MT_N - c);
+        }
+        mt_twist_wave_k<K>(src, dst, lane);
     }
     m.stale = 0;
     // the refilled words are read later by their owner lane of this same wave: order the stores before those loads
@@ -333,14 +336,16 @@ __device__ __forceinline__ void mt_refill_wave(M& m, int lane)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// STAGE_LDS rows: W bytes per lane (W multiple of 64). Row stride W + 16 (16-B copies persist the rows in HBM between
-// launches) or, for W >= 128, W + 8 with 8-B copies: Limit's occupancy is LDS-bound and stride 136 fits 3 blocks per
-// CU where 144 fit 2 (measured: Limit 1.405 -> 1.339 ms/launch; Leduc's W = 64 is 2 % faster at stride 80 than 72).
-template <int W>
+// STAGE_LDS rows: W bytes per lane (W multiple of 64), row stride W + PAD (per game): LDS bounds occupancy, so the
+// pad is as small as the measurements allow (steady-state A/B on MI355X: Leduc W 64 + 4 fits 6 blocks per CU and is
+// 13 % faster than W + 16; Limit W 128 + 8 fits 3 blocks per CU where + 16 fitted 2, and beats + 4 by 1.5 %). The
+// persist copies move 16 / 8 / 4 B per lane, whatever the stride allows.
+template <int W, int PAD>
 struct Stage {
     static_assert(W % WAVE == 0, "LDS staging rows are filled 64 words per wave instruction");
-    static constexpr int STRIDE = W >= 128 ? W + 8 : W + 16;
-    static constexpr int CHUNK = STRIDE % 16 == 0 ? 16 : 8;   // bytes per persist copy
+    static_assert(PAD % 4 == 0, "rows are written as dwords");
+    static constexpr int STRIDE = W + PAD;
+    static constexpr int CHUNK = STRIDE % 16 == 0 ? 16 : (STRIDE % 8 == 0 ? 8 : 4);   // bytes per persist copy
     static constexpr int BYTES = WAVE * STRIDE;
 };
 
@@ -355,10 +360,10 @@ __device__ __forceinline__ void wave_sync_lds()
 // loaded COALESCED by the whole wave (all 64 lanes read one lane's consecutive words), tempered and packed to bytes
 // (lanes 4q gather lanes 4q+1..3 with DPP row shifts: VALU, no LDS traffic). area = the wave's staging area (lane j's
 // row at area + j * STRIDE). All 64 lanes must call.
-template <int W, int R, int B>
+template <int W, int PAD, int R, int B>
 __device__ __forceinline__ void mt_restage_wave(MtLaneT<STAGE_LDS>& m, uint8_t* area, int lane)
 {
-    constexpr int STRIDE = Stage<W>::STRIDE, C = W / WAVE;
+    constexpr int STRIDE = Stage<W, PAD>::STRIDE, C = W / WAVE;
     m.stg = area + lane * STRIDE;
     const uint32_t k = m.staged_offset();
     uint64_t todo = __ballot(k >= m.sn || m.sn - k < (uint32_t)R);
@@ -408,10 +413,10 @@ __device__ __forceinline__ void mt_restage_wave(MtLaneT<STAGE_LDS>& m, uint8_t* 
 
 // Persist / restore a wave's staging rows (W bytes per env, HBM row-major [env][W]) with coalesced 16-B / 8-B copies, so a
 // launch does not restage every lane from scratch. nvalid = envs of this wave.
-template <int W>
+template <int W, int PAD>
 __device__ __forceinline__ void stage_rows_copy(uint8_t* area, uint8_t* hbm_rows, int lane, int nvalid, bool to_lds)
 {
-    constexpr int STRIDE = Stage<W>::STRIDE, CH = Stage<W>::CHUNK, CPR = W / CH;   // chunks per row
+    constexpr int STRIDE = Stage<W, PAD>::STRIDE, CH = Stage<W, PAD>::CHUNK, CPR = W / CH;   // chunks per row
 #pragma unroll
     for (int i = 0; i < CPR; i++) {
         const int q = i * WAVE + lane, row = q / CPR, col = q - row * CPR;
@@ -421,9 +426,12 @@ __device__ __forceinline__ void stage_rows_copy(uint8_t* area, uint8_t* hbm_rows
             if constexpr (CH == 16) {
                 if (to_lds) *(uint4*)l = *(const uint4*)g;
                 else *(uint4*)g = *(const uint4*)l;
-            } else {
+            } else if constexpr (CH == 8) {
                 if (to_lds) *(uint2*)l = *(const uint2*)g;
                 else *(uint2*)g = *(const uint2*)l;
+            } else {
+                if (to_lds) *(uint32_t*)l = *(const uint32_t*)g;
+                else *(uint32_t*)g = *(const uint32_t*)l;
             }
         }
     }

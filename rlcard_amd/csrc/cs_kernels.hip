@@ -78,10 +78,10 @@ __device__ __forceinline__ MtLaneT<MODE> mt_lane(uint32_t* mt, const uint32_t* c
     return m;
 }
 
-template <class M>
+template <class G, class M>
 __device__ __forceinline__ void refill(M& m, int lane, int flags)
 {
-    if (!(flags & 1)) mt_refill_wave(m, lane);
+    if (!(flags & 1)) mt_refill_wave<G::REFILL_K>(m, lane);
 }
 
 // obs rows: staged + coalesced when the row is a dword multiple, per-lane bytes otherwise
@@ -136,24 +136,24 @@ template <class G>
 struct ObsLds {
     static constexpr int WORDS = ObsWords<G::OBS, !G::RAW_OBS && G::OBS % 4 == 0>::value;
 };
-template <int W, bool LDS>
+template <int W, int PAD, bool LDS>
 struct StageBytesOf {
     static constexpr int value = 16;
 };
-template <int W>
-struct StageBytesOf<W, true> {
-    static constexpr int value = Stage<W>::BYTES;
+template <int W, int PAD>
+struct StageBytesOf<W, PAD, true> {
+    static constexpr int value = Stage<W, PAD>::BYTES;
 };
 template <class G>
 struct StageBytes {
-    static constexpr int value = StageBytesOf<G::STAGE_W, G::STAGE_MODE == STAGE_LDS>::value;
+    static constexpr int value = StageBytesOf<G::STAGE_W, G::STAGE_PAD, G::STAGE_MODE == STAGE_LDS>::value;
 };
 // restage after the refill, per the game's staging mode (see MtLaneT)
 template <class G, class M>
 __device__ __forceinline__ void restage(M& m, uint8_t* area, int lane)
 {
     if constexpr (G::STAGE_MODE == STAGE_REGS) m.template restage_regs<G::STAGE_R>();
-    else if constexpr (G::STAGE_MODE == STAGE_LDS) mt_restage_wave<G::STAGE_W, G::STAGE_R, G::RESTAGE_B>(m, area, lane);
+    else if constexpr (G::STAGE_MODE == STAGE_LDS) mt_restage_wave<G::STAGE_W, G::STAGE_PAD, G::STAGE_R, G::RESTAGE_B>(m, area, lane);
 }
 template <class G>
 struct Scratch {   // per-lane LDS words of games that keep state in LDS (blackjack); one word per wave otherwise
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, ui
         g.load(st, n, c.env);   // the Game object outlives init_game (limit-holdem's raise history, :98/:101)
         g.reset(m);
     }
-    refill(m, c.lane, flags & 1);
+    refill<G>(m, c.lane, flags & 1);
     uint32_t bits[G::NB];
     const int p = g.current();
     g.observe(p, bits);
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uin
             if (done) g.payoffs(r);
         }
     }
-    refill(m, c.lane, flags & 1);
+    refill<G>(m, c.lane, flags & 1);
     uint32_t bits[G::NB];
     const int p = g.current();
     g.observe(p, bits);
@@ -320,7 +320,7 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, 
                 m.sp = w & 0xFFFFu;
                 m.sn = w >> 16;
             }
-            stage_rows_copy<G::STAGE_W>(stage[c.wid], rows, c.lane, c.nvalid, true);
+            stage_rows_copy<G::STAGE_W, G::STAGE_PAD>(stage[c.wid], rows, c.lane, c.nvalid, true);
         }
     }
     G g;
@@ -330,7 +330,7 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, 
         g.load(st, n, c.env);
         if (g.is_over()) g.reset(m);
     }
-    refill(m, c.lane, flags & 1);
+    refill<G>(m, c.lane, flags & 1);
     if (staged) restage<G>(m, stage[c.wid], c.lane);
     uint8_t* obs = (uint8_t*)out.obs;
     uint8_t* legal = (uint8_t*)out.legal;
@@ -364,13 +364,13 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, 
             done_o[row] = (uint8_t)done;
             if (done) g.reset(m);
         }
-        refill(m, c.lane, flags & 1);
+        refill<G>(m, c.lane, flags & 1);
         if (staged) restage<G>(m, stage[c.wid], c.lane);
     }
     bool keep = false;
     if constexpr (persist) {
         if (staged) {
-            stage_rows_copy<G::STAGE_W>(stage[c.wid], rows, c.lane, c.nvalid, false);
+            stage_rows_copy<G::STAGE_W, G::STAGE_PAD>(stage[c.wid], rows, c.lane, c.nvalid, false);
             keep = true;
         }
     }

@@ -15,6 +15,12 @@
 #pragma once
 #include "cs_device.h"
 
+#ifndef CS_LEDUC_RESTAGE_B
+#define CS_LEDUC_RESTAGE_B 4
+#endif
+#ifndef CS_LEDUC_REFILL_K
+#define CS_LEDUC_REFILL_K 1
+#endif
 #ifndef CS_LEDUC_STAGE_R
 
 #define CS_LEDUC_STAGE_R 12
@@ -27,8 +33,10 @@ struct Leduc {
     static constexpr int NB = 2;  // obs bitmap words
     static constexpr bool RAW_OBS = false;
     static constexpr int SCRATCH_WORDS = 0;
-    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 64, STAGE_R = CS_LEDUC_STAGE_R;  // MT staging (see MtLaneT)
-    static constexpr int RESTAGE_B = 4;  // lanes restaged per pass (loads in flight), measured: 4 > 8 > 1
+    // MT staging (see MtLaneT)
+    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 64, STAGE_PAD = 4, STAGE_R = CS_LEDUC_STAGE_R;
+    static constexpr int RESTAGE_B = CS_LEDUC_RESTAGE_B;  // lanes restaged per pass (loads in flight): 4 > 8 > 1
+    static constexpr int REFILL_K = CS_LEDUC_REFILL_K;    // 1: refills are rare here, and K = 2 costs 12 VGPRs = 1 wave/SIMD
     __device__ __forceinline__ void bind(uint32_t*, const GameParams&) {}
     enum { CALL = 0, RAISE = 1, FOLD = 2, CHECK = 3 };
 

@@ -1,5 +1,8 @@
 """A/B timing of k_rollout kernel variants (cs_debug_set_kernel_flags) interleaved in ONE process (rule 24).
-  python tools/ab_rollout.py GAME N T flagsA flagsB ..."""
+  python tools/ab_rollout.py GAME N T flagsA flagsB ...
+AB_WARM (env, default 40) launches run first so the MT streams reach their steady block-refill rate (every env starts
+at stream position 0 after seeding, so the first refills all come ~624 draws in)."""
+import os
 import sys
 import statistics
 
@@ -14,6 +17,8 @@ v = VecEnv(game, n, seed=42, device=0)
 v.reset()
 tr = v.new_traj_out(T)
 t = 0
+for _ in range(int(os.environ.get('AB_WARM', '40'))):
+    v.rollout(T, 5, t * T, out=tr); t += 1
 for f in variants:            # warm-up each variant
     v.set_kernel_flags(f)
     v.rollout(T, 5, t * T, out=tr); t += 1
