@@ -101,17 +101,16 @@ __device__ __forceinline__ uint32_t* lane_ptr(uint32_t* p, int j)
 
 // One lane's view of its env's stream. MODE selects how draws are served:
 //   STAGE_NONE  one global load per draw (single-step kernels: staging would cost more than it saves);
-//   STAGE_REGS  16 staged bytes in 4 VGPRs (Leduc: a reset needs ~7 draws);
-//   STAGE_LDS   W staged bytes in a per-lane LDS row (Limit / Blackjack: a reset needs ~72-80 draws).
+//   STAGE_LDS   W staged bytes in a per-lane LDS row (the rollout kernels).
 // Why staging: lanes sit at different stream positions, so one load per draw is a 64-line gather per wave
 // instruction, and a reset's rejection loops issue one such gather per trip of the slowest lane (rocprofv3 on
 // k_rollout<Leduc>: TA busy 68% of the kernel, ~300 L1 accesses per wave-step, waves waiting 80% of their cycles).
 // Every draw of this engine is random_interval(max <= 53), which looks only at the low 8 bits of the tempered word,
 // so at step boundaries (after the refill: both blocks valid) lanes running low restage their next words, temper
-// them and keep the low bytes; draws then read registers / LDS, global only as a fallback when a lane outruns its
-// stage. Measured on MI355X (tools/ab_rollout.py): a per-draw 8-word register window was 1.6x slower and 8/16-word
-// register bursts inside the reset +3% / 2.7x slower than one load per draw.
-enum { STAGE_NONE = 0, STAGE_REGS = 1, STAGE_LDS = 2 };
+// them and keep the low bytes; draws then read LDS, global only as a fallback when a lane outruns its stage.
+// Measured on MI355X (tools/ab_rollout.py): staging beat one load per draw by 13-30 %; register variants (a per-draw
+// 8-word window, 8/16-word bursts inside the reset, 16 staged bytes in 4 VGPRs) all lost to it.
+enum { STAGE_NONE = 0, STAGE_LDS = 2 };
 
 template <int MODE = STAGE_NONE>
 struct MtLaneT {
@@ -119,7 +118,6 @@ struct MtLaneT {
     uint32_t pos;
     uint32_t stale;
     uint32_t sp, sn;            // stream position of staged byte 0; staged bytes
-    uint32_t s0, s1, s2, s3;    // STAGE_REGS: 16 staged bytes
     const uint8_t* stg;         // STAGE_LDS: this lane's row
 
     __device__ __forceinline__ void init(uint32_t* p_base, uint32_t p, uint32_t s)
@@ -129,7 +127,6 @@ struct MtLaneT {
         stale = s;
         sp = 0;
         sn = 0;
-        s0 = s1 = s2 = s3 = 0;
         stg = nullptr;
     }
 
@@ -162,12 +159,7 @@ struct MtLaneT {
         } else {
             const uint32_t k = staged_offset();
             if (k < sn) {
-                if constexpr (MODE == STAGE_REGS) {
-                    const uint32_t w = k < 8 ? (k < 4 ? s0 : s1) : (k < 12 ? s2 : s3);
-                    v = (w >> (8 * (k & 3))) & 255u;
-                } else {
-                    v = stg[k];
-                }
+                v = stg[k];
             } else {
                 v = mt_temper(base[pos]) & 255u;
             }
@@ -236,30 +228,6 @@ struct MtLaneT {
             advance_by(k - k0);
         }
         for (; i >= 1; i--) (void)interval(i);
-    }
-
-    // STAGE_REGS restage (per lane, no cross-lane work): a lane with fewer than R staged draws left loads the
-    // 16-word chunk starting at pos & ~3 (four 16-B loads, wrapping at the end of the 1248-word ring), tempers it and
-    // keeps the low bytes. All needy lanes load in the same wave instructions.
-    template <int R>
-    __device__ __forceinline__ void restage_regs()
-    {
-        const uint32_t k = staged_offset();
-        if (k >= sn || sn - k < (uint32_t)R) {
-            const uint32_t a = pos & ~3u;
-            uint32_t w[4];
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                uint32_t q = a + 4u * c;
-                if (q >= (uint32_t)MT_WORDS) q -= MT_WORDS;
-                const uint4 x = *(const uint4*)(base + q);
-                w[c] = (mt_temper(x.x) & 255u) | (mt_temper(x.y) & 255u) << 8 | (mt_temper(x.z) & 255u) << 16 |
-                       (mt_temper(x.w) & 255u) << 24;
-            }
-            s0 = w[0]; s1 = w[1]; s2 = w[2]; s3 = w[3];
-            sp = a;
-            sn = 16;
-        }
     }
 };
 using MtLane = MtLaneT<STAGE_NONE>;

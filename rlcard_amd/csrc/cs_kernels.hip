@@ -152,8 +152,7 @@ struct StageBytes {
 template <class G, class M>
 __device__ __forceinline__ void restage(M& m, uint8_t* area, int lane)
 {
-    if constexpr (G::STAGE_MODE == STAGE_REGS) m.template restage_regs<G::STAGE_R>();
-    else if constexpr (G::STAGE_MODE == STAGE_LDS) mt_restage_wave<G::STAGE_W, G::STAGE_PAD, G::STAGE_R, G::RESTAGE_B>(m, area, lane);
+    if constexpr (G::STAGE_MODE == STAGE_LDS) mt_restage_wave<G::STAGE_W, G::STAGE_PAD, G::STAGE_R, G::RESTAGE_B>(m, area, lane);
 }
 template <class G>
 struct Scratch {   // per-lane LDS words of games that keep state in LDS (blackjack); one word per wave otherwise
