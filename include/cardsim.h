@@ -48,7 +48,8 @@ typedef struct {
     int32_t legal_bytes;  /* ceil(num_actions / 8): legal-action bitmask bytes per row */
     int32_t action_bytes; /* dtype width of rollout action rows: 1 (uint8) or 2 (int16, doudizhu) */
     int32_t state_words;  /* packed u32 words of game state per env */
-    int32_t reserved[2];
+    int32_t action_feature_dim; /* bytes per cs_action_features row: doudizhu 54, otherwise num_actions (one-hot) */
+    int32_t reserved;
 } cs_game_info;
 
 /* Outputs of reset/step/observe, all device pointers, one row per env:
@@ -68,7 +69,9 @@ typedef struct {
 
 /* Rollout trajectory, all device pointers, rows [T][n]:
  *   obs [T][n][obs_dim] u8, legal [T][n][legal_bytes] u8, player [T][n] u8 (the acting player's pre-step view),
- *   action [T][n] (uint8 or int16 per cs_game_info.action_bytes), reward [T][n][num_players] f32, done [T][n] u8. */
+ *   action [T][n] (uint8 or int16 per cs_game_info.action_bytes), reward [T][n][num_players] f32, done [T][n] u8,
+ *   final_obs [T][n][num_players][obs_dim] u8 OPTIONAL (NULL = skip): where done[t][e] = 1, every player's observation
+ *   of the finished game (the final states Env.run appends, envs/env.py:161-164); other rows are not written. */
 typedef struct {
     void* obs;
     void* legal;
@@ -76,7 +79,23 @@ typedef struct {
     void* action;
     void* reward;
     void* done;
+    void* final_obs;
 } cs_traj_out;
+
+/* Transitions of a rollout trajectory, all device pointers [T][n] (any may be NULL to skip it):
+ *   next_t i32   row of the acting player's next observation in the same game (obs[next_t][e]); -1 = the game ended
+ *                first (next state = final_obs[end_t][e][player]); -2 = the game continues past the window
+ *   end_t  i32   row where the row's game ends, -1 = past the window
+ *   reward f32   the acting player's payoff on its last transition of the game, else 0
+ *   done   u8    1 on that last transition
+ *   ret    f32   the acting player's payoff of the game (DMC target), NaN if the game ends past the window */
+typedef struct {
+    void* next_t;
+    void* end_t;
+    void* reward;
+    void* done;
+    void* ret;
+} cs_trans_out;
 
 /* Shape of a game under a config. Replaces reading Env.num_players / num_actions / state_shape. */
 int cs_game_info_get(int32_t game, const cs_config* cfg, cs_game_info* info);
@@ -110,6 +129,21 @@ int cs_observe(cs_handle* h, int32_t player, const cs_step_out* out, void* strea
  * Replaces T iterations of the Env.run loop (envs/env.py:120-169) for every env. */
 int cs_rollout(cs_handle* h, int32_t T, uint64_t policy_seed, uint64_t t0, uint64_t env_base, const cs_traj_out* out,
                void* stream);
+
+/* rlcard's reorganize (utils/utils.py:153-179: per player [state, action, reward, next_state, done]) and the DMC
+ * return target (agents/dmc_agent/utils.py:97-163) of a cs_rollout trajectory of this handle, on the device. `traj`
+ * needs player, reward and done. Games still running at the end of the window come out as next_t = -2. */
+int cs_transitions(cs_handle* h, int32_t T, const cs_traj_out* traj, const cs_trans_out* out, void* stream);
+
+/* Legal-action id lists of `rows` legal bitmask rows of this game (wavefront compaction; the keys of
+ * state['legal_actions']): counts i32 [rows], offsets i64 [rows + 1] (exclusive prefix sum, offsets[rows] = total),
+ * ids i32 [total] ascending per row. ids may be NULL: size it from offsets[rows], then call again with it. */
+int cs_legal_lists(cs_handle* h, const void* legal, int64_t rows, int32_t* counts, int64_t* offsets, int32_t* ids,
+                   void* stream);
+
+/* Action features of `count` action ids (Env.get_action_feature: doudizhu _cards2array of the combo, 54 B,
+ * envs/doudizhu.py:136-142; other games one-hot of num_actions, envs/env.py:211-220): u8 [count][action_feature_dim]. */
+int cs_action_features(cs_handle* h, const int32_t* ids, int64_t count, void* features, void* stream);
 
 /* Copy the packed state words of env `env` (state_words u32, HOST buffer) -- the raw fields behind
  * Env.get_state()['raw_obs'] / get_perfect_information for single-env compatibility and debugging. Synchronous. */

@@ -116,7 +116,7 @@ void or_batch_observe(or_batch *b, int64_t env, int player, uint8_t *obs, uint8_
 
 void or_batch_rollout(or_batch *b, int32_t T, uint64_t policy_seed, uint64_t t0, uint64_t env_base,
                       uint8_t *obs, uint8_t *legal, uint8_t *player, int32_t *action, float *reward,
-                      uint8_t *done)
+                      uint8_t *done, uint8_t *final_obs)
 {
     const int64_t n = b->n;
     const int O = b->info.obs_dim, LB = b->info.legal_bytes, P = b->info.num_players;
@@ -138,6 +138,13 @@ void or_batch_rollout(or_batch *b, int32_t T, uint64_t policy_seed, uint64_t t0,
             done[row] = (uint8_t)b->vt->is_over(e);
             if (done[row]) {
                 b->vt->payoffs(e, &b->rng[i], r);
+                if (final_obs) {   /* Env.run's final state of every player (envs/env.py:161-164) */
+                    uint8_t scratch[4096];
+                    for (int p = 0; p < P; p++) {
+                        memset(scratch, 0, (size_t)LB);
+                        b->vt->observe(e, p, final_obs + (row * P + p) * O, scratch);
+                    }
+                }
                 b->vt->init_game(e, &b->rng[i], &b->cfg);
             }
         }

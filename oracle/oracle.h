@@ -74,8 +74,8 @@ void or_batch_step(or_batch *b, const int32_t *actions, uint8_t *obs, uint8_t *l
                    float *reward, uint8_t *done);
 void or_batch_observe(or_batch *b, int64_t env, int player, uint8_t *obs, uint8_t *legal);
 void or_batch_rollout(or_batch *b, int32_t T, uint64_t policy_seed, uint64_t t0, uint64_t env_base,
-                      uint8_t *obs, uint8_t *legal, uint8_t *player, int32_t *action, float *reward,
-                      uint8_t *done);
+                      uint8_t *obs, uint8_t *legal, uint8_t *player, int32_t *action, float *reward, uint8_t *done,
+                      uint8_t *final_obs /* [T][n][P][obs_dim] at done rows, or NULL */);
 /* total u32 draws consumed so far by env i (for RNG-position parity checks) */
 uint64_t or_batch_draws(or_batch *b, int64_t env);
 

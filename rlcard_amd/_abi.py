@@ -21,7 +21,7 @@ class Config(C.Structure):
 class GameInfo(C.Structure):
     _fields_ = [('obs_dim', C.c_int32), ('num_actions', C.c_int32), ('num_players', C.c_int32),
                 ('legal_bytes', C.c_int32), ('action_bytes', C.c_int32), ('state_words', C.c_int32),
-                ('reserved', C.c_int32 * 2)]
+                ('action_feature_dim', C.c_int32), ('reserved', C.c_int32)]
 
 
 class StepOut(C.Structure):
@@ -31,12 +31,17 @@ class StepOut(C.Structure):
 
 class TrajOut(C.Structure):
     _fields_ = [('obs', C.c_void_p), ('legal', C.c_void_p), ('player', C.c_void_p), ('action', C.c_void_p),
-                ('reward', C.c_void_p), ('done', C.c_void_p)]
+                ('reward', C.c_void_p), ('done', C.c_void_p), ('final_obs', C.c_void_p)]
+
+
+class TransOut(C.Structure):
+    _fields_ = [('next_t', C.c_void_p), ('end_t', C.c_void_p), ('reward', C.c_void_p), ('done', C.c_void_p),
+                ('ret', C.c_void_p)]
 
 
 # every symbol include/cardsim.h declares (tests check the library exports all of them)
 SYMBOLS = ('cs_game_info_get', 'cs_create', 'cs_destroy', 'cs_seed', 'cs_reset', 'cs_step', 'cs_observe',
-           'cs_rollout', 'cs_get_env_state', 'cs_get_rng_ctl', 'cs_debug_set_serial_refill', 'cs_debug_set_kernel_flags',
+           'cs_rollout', 'cs_transitions', 'cs_legal_lists', 'cs_action_features', 'cs_get_env_state', 'cs_get_rng_ctl', 'cs_debug_set_serial_refill', 'cs_debug_set_kernel_flags',
            'cs_last_error', 'cs_version')
 
 _lib = None
@@ -64,6 +69,9 @@ def lib():
     L.cs_step.argtypes = [vp, vp, C.POINTER(StepOut), vp]
     L.cs_observe.argtypes = [vp, i32, C.POINTER(StepOut), vp]
     L.cs_rollout.argtypes = [vp, i32, u64, u64, u64, C.POINTER(TrajOut), vp]
+    L.cs_transitions.argtypes = [vp, i32, C.POINTER(TrajOut), C.POINTER(TransOut), vp]
+    L.cs_legal_lists.argtypes = [vp, vp, i64, vp, vp, vp, vp]
+    L.cs_action_features.argtypes = [vp, vp, i64, vp, vp]
     L.cs_get_env_state.argtypes = [vp, i64, vp, i32]
     L.cs_get_rng_ctl.argtypes = [vp, i64, vp]
     L.cs_debug_set_serial_refill.argtypes = [vp, i32]
@@ -71,7 +79,7 @@ def lib():
     L.cs_last_error.restype = C.c_char_p
     L.cs_version.restype = C.c_char_p
     for name in ('cs_game_info_get', 'cs_create', 'cs_seed', 'cs_reset', 'cs_step', 'cs_observe', 'cs_rollout',
-                 'cs_get_env_state', 'cs_get_rng_ctl', 'cs_debug_set_serial_refill', 'cs_debug_set_kernel_flags'):
+                 'cs_transitions', 'cs_legal_lists', 'cs_action_features', 'cs_get_env_state', 'cs_get_rng_ctl', 'cs_debug_set_serial_refill', 'cs_debug_set_kernel_flags'):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

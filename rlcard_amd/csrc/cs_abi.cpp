@@ -21,6 +21,8 @@ struct cs_handle {
     bool seeded;
     void* table_dev;     // doudizhu: device action table (one allocation)
     cs::ddz::Tab tab;    // doudizhu: views into it, passed to the kernels by value
+    void* scan_tmp;      // cs_legal_lists: prefix-scan scratch, grown on demand
+    size_t scan_bytes;
 };
 
 namespace {
@@ -121,6 +123,7 @@ void cs_destroy(cs_handle* h)
     if (h->b.sctl) (void)hipFree(h->b.sctl);
     if (h->b.sbuf) (void)hipFree(h->b.sbuf);
     if (h->table_dev) (void)hipFree(h->table_dev);
+    if (h->scan_tmp) (void)hipFree(h->scan_tmp);
     delete h;
 }
 
@@ -197,6 +200,41 @@ int cs_rollout(cs_handle* h, int32_t T, uint64_t policy_seed, uint64_t t0, uint6
     if (r != CS_OK) return r;
     hipError_t e = cs::launch_rollout(h->b, T, policy_seed, t0, env_base, *out, (hipStream_t)stream);
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_rollout");
+}
+
+int cs_transitions(cs_handle* h, int32_t T, const cs_traj_out* traj, const cs_trans_out* out, void* stream)
+{
+    if (!h || !traj || !out) return fail(CS_E_INVALID, "null argument");
+    if (!traj->player || !traj->reward || !traj->done) return fail(CS_E_INVALID, "traj needs player, reward and done");
+    if (T <= 0) return fail(CS_E_INVALID, "T must be positive");
+    int r = set_device(h);
+    if (r != CS_OK) return r;
+    hipError_t e = cs::launch_transitions(h->b, T, *traj, *out, (hipStream_t)stream);
+    return e == hipSuccess ? CS_OK : fail_hip(e, "cs_transitions");
+}
+
+int cs_legal_lists(cs_handle* h, const void* legal, int64_t rows, int32_t* counts, int64_t* offsets, int32_t* ids,
+                   void* stream)
+{
+    if (!h || !legal || !counts || !offsets) return fail(CS_E_INVALID, "null argument");
+    if (rows <= 0 || rows > ((int64_t)1 << 31) - 1) return fail(CS_E_INVALID, "rows out of range");
+    int r = set_device(h);
+    if (r != CS_OK) return r;
+    hipError_t e = cs::launch_legal_lists(h->b, h->info.legal_bytes, (const uint8_t*)legal, rows, counts, offsets, ids,
+                                          &h->scan_tmp, &h->scan_bytes, (hipStream_t)stream);
+    return e == hipSuccess ? CS_OK : fail_hip(e, "cs_legal_lists");
+}
+
+int cs_action_features(cs_handle* h, const int32_t* ids, int64_t count, void* features, void* stream)
+{
+    if (!h || !ids || !features) return fail(CS_E_INVALID, "null argument");
+    if (count <= 0) return fail(CS_E_INVALID, "count must be positive");
+    int r = set_device(h);
+    if (r != CS_OK) return r;
+    hipError_t e = h->b.game == CS_GAME_DOUDIZHU
+                       ? cs::ddz::launch_features(h->b, ids, count, (uint8_t*)features, (hipStream_t)stream)
+                       : cs::launch_onehot(ids, count, h->info.num_actions, (uint8_t*)features, (hipStream_t)stream);
+    return e == hipSuccess ? CS_OK : fail_hip(e, "cs_action_features");
 }
 
 int cs_get_env_state(cs_handle* h, int64_t env, uint32_t* host_words, int32_t nwords)

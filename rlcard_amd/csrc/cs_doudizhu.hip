@@ -724,13 +724,43 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, 
             o[0] = r[0]; o[1] = r[1]; o[2] = r[2];
             ((uint8_t*)out.done)[row] = (uint8_t)done;
         }
-        if (done) deal(e, m, lane);
+        if (done) {
+            if (out.final_obs) {   // Env.run's final state of every player (envs/env.py:161-164)
+                for (uint32_t q = 0; q < (uint32_t)P; q++) {
+                    wave_sync_lds();
+                    build_obs(e, q, L, lane);
+                    wave_sync_lds();
+                    write_obs_row(L, (uint8_t*)out.final_obs + (row * P + q) * OBS, lane);
+                }
+            }
+            deal(e, m, lane);
+        }
     }
     e.store(st, c.env, lane);
     if (lane == 0) ctl[c.env] = m.pos | (m.stale << 16);
 }
 
+// _cards2array of action ids (envs/doudizhu.py:136-142 get_action_feature; pass and invalid ids -> zeros), one
+// thread per id, 27 two-byte stores per 54-byte row
+__global__ __launch_bounds__(BLOCK) void k_features(const int32_t* __restrict__ ids, int64_t count, uint8_t* out, Tab tb)
+{
+    const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= count) return;
+    const int32_t id = ids[i];
+    const uint64_t bits = cards_bits(id >= 0 && id < PASS ? tb.cnt[id] : 0ull);
+    uint16_t* o = (uint16_t*)(out + i * 54);
+#pragma unroll
+    for (int k = 0; k < 27; k++) o[k] = (uint16_t)(((bits >> (2 * k)) & 1u) | (((bits >> (2 * k + 1)) & 1u) << 8));
+}
+
 static inline dim3 grid_of(int64_t n) { return dim3((unsigned)((n + WPB - 1) / WPB)); }
+
+hipError_t launch_features(const Buffers& b, const int32_t* ids, int64_t count, uint8_t* out, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_features, dim3((unsigned)((count + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, ids, count, out,
+                       *(const Tab*)b.table);
+    return hipGetLastError();
+}
 
 hipError_t launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s)
 {

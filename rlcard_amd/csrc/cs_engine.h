@@ -33,12 +33,20 @@ hipError_t launch_observe(const Buffers& b, int32_t player, const cs_step_out& o
 hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
                           const cs_traj_out& o, hipStream_t s);
 
+// cs_traj.hip
+hipError_t launch_transitions(const Buffers& b, int32_t T, const cs_traj_out& tr, const cs_trans_out& o,
+                              hipStream_t s);
+hipError_t launch_legal_lists(const Buffers& b, int32_t lb, const uint8_t* legal, int64_t rows, int32_t* counts,
+                              int64_t* offsets, int32_t* ids, void** tmp, size_t* tmp_bytes, hipStream_t s);
+hipError_t launch_onehot(const int32_t* ids, int64_t count, int32_t na, uint8_t* out, hipStream_t s);
+
 namespace ddz {   // cs_doudizhu.hip (seeding goes through the shared k_seed)
 hipError_t launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s);
 hipError_t launch_step(const Buffers& b, const int32_t* actions, const cs_step_out& o, hipStream_t s);
 hipError_t launch_observe(const Buffers& b, int32_t player, const cs_step_out& o, hipStream_t s);
 hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
                           const cs_traj_out& o, hipStream_t s);
+hipError_t launch_features(const Buffers& b, const int32_t* ids, int64_t count, uint8_t* out, hipStream_t s);
 }  // namespace ddz
 
 }  // namespace cs

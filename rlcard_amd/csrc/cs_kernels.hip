@@ -106,6 +106,23 @@ __device__ __forceinline__ void emit_obs(uint32_t* lds, const uint32_t (&bits)[G
     }
 }
 
+// one obs row straight from a lane (final observations: only the lanes whose game just ended write)
+template <class G>
+__device__ __forceinline__ void write_obs_direct(uint8_t* o, const uint32_t (&bits)[G::NB])
+{
+    if constexpr (G::RAW_OBS) {
+#pragma unroll
+        for (int k = 0; k < G::OBS; k++) o[k] = (uint8_t)(bits[k >> 2] >> (8 * (k & 3)));
+    } else if constexpr (G::OBS % 4 == 0) {
+#pragma unroll
+        for (int j = 0; j < G::OBS / 4; j++)
+            ((uint32_t*)o)[j] = RowWriter<G::OBS>::expand4(bits[j / 8] >> (4 * (j % 8)));
+    } else {
+#pragma unroll
+        for (int k = 0; k < G::OBS; k++) o[k] = (uint8_t)((bits[k >> 5] >> (k & 31)) & 1u);
+    }
+}
+
 template <class G>
 __device__ __forceinline__ void emit_legal(uint8_t* legal, int64_t row, uint64_t lg)
 {
@@ -358,7 +375,17 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, 
             else ((int16_t*)out.action)[row] = (int16_t)a;
             g.step(a, m);
             done = g.is_over();
-            if (done) g.payoffs(r);
+            if (done) {
+                g.payoffs(r);
+                if (out.final_obs) {   // Env.run's final state of every player (envs/env.py:161-164)
+#pragma unroll
+                    for (int q = 0; q < G::P; q++) {
+                        uint32_t fb[G::NB];
+                        g.observe(q, fb);
+                        write_obs_direct<G>((uint8_t*)out.final_obs + (row * G::P + q) * G::OBS, fb);
+                    }
+                }
+            }
             emit_reward<G>(reward, row, r);
             done_o[row] = (uint8_t)done;
             if (done) g.reset(m);
@@ -429,6 +456,7 @@ static void fill_info(cs_game_info* info)
     info->legal_bytes = G::LB;
     info->action_bytes = G::ACTION_BYTES;
     info->state_words = G::WORDS;
+    info->action_feature_dim = G::A;
 }
 
 template <class G>
@@ -473,6 +501,7 @@ int game_info(int32_t game, const cs_config* cfg, cs_game_info* info)
         info->legal_bytes = ddz::LB;
         info->action_bytes = 2;
         info->state_words = ddz::WORDS;
+        info->action_feature_dim = 54;
         return CS_OK;
     default:
         return CS_E_UNSUPPORTED;

@@ -1,0 +1,189 @@
+// cs_traj.hip -- the steps right after the rollout, on the device:
+//   k_transitions                  rlcard's reorganize (rlcard/utils/utils.py:153-179) + the DMC return target
+//                                  (rlcard/agents/dmc_agent/utils.py:97-163) for every (step, env) of a trajectory
+//   k_legal_count / k_legal_fill   legal-action id lists from the bitmask rows (wavefront compaction), the form the
+//                                  agents consume (state['legal_actions'] keys, envs/env.py _extract_state)
+// All HBM-bound streaming: a few bytes per row in and out.
+#include <hipcub/hipcub.hpp>
+#include "cs_device.h"
+#include "cs_engine.h"
+
+namespace cs {
+
+constexpr int TBLOCK = 256;
+constexpr int MAXP = 4;
+
+// One lane per env, scanning its T rows backwards. Row (t, e) is a transition of the player who acted at t:
+//   next_t  its next turn in the same game, -1 = the game ended first (next state = final_obs at row end_t), -2 = the
+//           game goes on past the window (the caller carries it into the next chunk)
+//   end_t   row where this row's game ends, -1 = past the window
+//   reward  the player's payoff on its last transition of the game, else 0 (reorganize: payoffs[player], done True)
+//   done    1 on that last transition
+//   ret     the player's payoff of the game (the DMC target for every step it took), NaN if the game ends past the window
+__global__ __launch_bounds__(TBLOCK) void k_transitions(const uint8_t* __restrict__ player,
+                                                        const uint8_t* __restrict__ done,
+                                                        const float* __restrict__ reward, int T, int64_t n, int P,
+                                                        int32_t* next_t, int32_t* end_t, float* r_out, uint8_t* d_out,
+                                                        float* ret)
+{
+    const int64_t e = (int64_t)blockIdx.x * TBLOCK + threadIdx.x;
+    if (e >= n) return;
+    const float nan = __builtin_nanf("");
+    int32_t nxt[MAXP];
+    float pay[MAXP];
+#pragma unroll
+    for (int q = 0; q < MAXP; q++) {
+        nxt[q] = -2;
+        pay[q] = nan;
+    }
+    int32_t end = -1;
+    for (int t = T - 1; t >= 0; t--) {
+        const int64_t row = (int64_t)t * n + e;
+        if (done[row]) {   // a game ends at t: rows t, t-1, ... back to the previous end belong to it
+            end = t;
+#pragma unroll
+            for (int q = 0; q < MAXP; q++) {
+                nxt[q] = -1;
+                pay[q] = q < P ? reward[row * P + q] : 0.f;
+            }
+        }
+        const int p = player[row];
+        int32_t np = -2;
+        float pp = nan;
+#pragma unroll
+        for (int q = 0; q < MAXP; q++) {
+            if (q == p) {
+                np = nxt[q];
+                pp = pay[q];
+                nxt[q] = t;
+            }
+        }
+        if (next_t) next_t[row] = np;
+        if (end_t) end_t[row] = end;
+        if (r_out) r_out[row] = np == -1 ? pp : 0.f;
+        if (d_out) d_out[row] = np == -1 ? 1 : 0;
+        if (ret) ret[row] = end >= 0 ? pp : nan;
+    }
+}
+
+// ---- legal lists ------------------------------------------------------------------------------------------------
+// short rows (<= 16 bytes: leduc / limit / blackjack): one lane per row
+__global__ __launch_bounds__(TBLOCK) void k_legal_count_small(const uint8_t* __restrict__ legal, int64_t rows, int lb,
+                                                              int32_t* counts)
+{
+    const int64_t r = (int64_t)blockIdx.x * TBLOCK + threadIdx.x;
+    if (r >= rows) return;
+    int c = 0;
+    for (int k = 0; k < lb; k++) c += __popc(legal[r * lb + k]);
+    counts[r] = c;
+}
+
+__global__ __launch_bounds__(TBLOCK) void k_legal_fill_small(const uint8_t* __restrict__ legal, int64_t rows, int lb,
+                                                             const int64_t* __restrict__ offsets, int32_t* ids)
+{
+    const int64_t r = (int64_t)blockIdx.x * TBLOCK + threadIdx.x;
+    if (r >= rows) return;
+    int64_t o = offsets[r];
+    for (int k = 0; k < lb; k++) {
+        uint32_t b = legal[r * lb + k];
+        while (b) {
+            ids[o++] = 8 * k + __builtin_ctz(b);
+            b &= b - 1;
+        }
+    }
+}
+
+// long rows (doudizhu: 3 434 bytes): one wave per row, lane l owns a contiguous slice of the row's bytes so the
+// ids come out ascending after a wave prefix scan of the per-lane counts
+template <bool FILL>
+__global__ __launch_bounds__(TBLOCK) void k_legal_wave(const uint8_t* __restrict__ legal, int64_t rows, int lb,
+                                                       int32_t* counts, const int64_t* __restrict__ offsets,
+                                                       int32_t* ids)
+{
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t r = (int64_t)blockIdx.x * (TBLOCK / WAVE) + threadIdx.x / WAVE;
+    if (r >= rows) return;
+    const uint8_t* row = legal + r * lb;
+    const int per = (lb + WAVE - 1) / WAVE, k0 = lane * per, k1 = k0 + per < lb ? k0 + per : lb;
+    int c = 0;
+    for (int k = k0; k < k1; k++) c += __popc(row[k]);
+    if constexpr (!FILL) {
+        for (int o = WAVE / 2; o; o >>= 1) c += __shfl_xor(c, o);
+        if (lane == 0) counts[r] = c;
+    } else {
+        int inc = c;
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const int y = __shfl_up(inc, o);
+            if (lane >= o) inc += y;
+        }
+        int64_t w = offsets[r] + (inc - c);
+        for (int k = k0; k < k1; k++) {
+            uint32_t b = row[k];
+            while (b) {
+                ids[w++] = 8 * k + __builtin_ctz(b);
+                b &= b - 1;
+            }
+        }
+    }
+}
+
+hipError_t launch_transitions(const Buffers& b, int32_t T, const cs_traj_out& tr, const cs_trans_out& o,
+                              hipStream_t s)
+{
+    hipLaunchKernelGGL(k_transitions, dim3((unsigned)((b.n + TBLOCK - 1) / TBLOCK)), dim3(TBLOCK), 0, s,
+                       (const uint8_t*)tr.player, (const uint8_t*)tr.done, (const float*)tr.reward, T, b.n,
+                       b.num_players, (int32_t*)o.next_t, (int32_t*)o.end_t, (float*)o.reward, (uint8_t*)o.done,
+                       (float*)o.ret);
+    return hipGetLastError();
+}
+
+hipError_t launch_legal_lists(const Buffers& b, int32_t lb, const uint8_t* legal, int64_t rows, int32_t* counts,
+                              int64_t* offsets, int32_t* ids, void** tmp, size_t* tmp_bytes, hipStream_t s)
+{
+    hipError_t e;
+    const bool wave = lb > 16;
+    const dim3 g_lane((unsigned)((rows + TBLOCK - 1) / TBLOCK)), g_wave((unsigned)((rows + 3) / 4));
+    if (wave) hipLaunchKernelGGL(k_legal_wave<false>, g_wave, dim3(TBLOCK), 0, s, legal, rows, lb, counts, nullptr,
+                                 nullptr);
+    else hipLaunchKernelGGL(k_legal_count_small, g_lane, dim3(TBLOCK), 0, s, legal, rows, lb, counts);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // offsets[0] = 0, offsets[1..rows] = inclusive prefix sum of the counts
+    if ((e = hipMemsetAsync(offsets, 0, sizeof(int64_t), s)) != hipSuccess) return e;
+    size_t need = 0;
+    if ((e = hipcub::DeviceScan::InclusiveSum(nullptr, need, counts, offsets + 1, rows, s)) != hipSuccess) return e;
+    if (need > *tmp_bytes) {
+        if (*tmp) (void)hipFree(*tmp);
+        *tmp = nullptr;
+        *tmp_bytes = 0;
+        if ((e = hipMalloc(tmp, need)) != hipSuccess) return e;
+        *tmp_bytes = need;
+    }
+    if ((e = hipcub::DeviceScan::InclusiveSum(*tmp, need, counts, offsets + 1, rows, s)) != hipSuccess) return e;
+    if (ids) {
+        if (wave) hipLaunchKernelGGL(k_legal_wave<true>, g_wave, dim3(TBLOCK), 0, s, legal, rows, lb, nullptr, offsets,
+                                     ids);
+        else hipLaunchKernelGGL(k_legal_fill_small, g_lane, dim3(TBLOCK), 0, s, legal, rows, lb, offsets, ids);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// one-hot action features (envs/env.py get_action_feature) for games without a card-combo feature
+__global__ __launch_bounds__(TBLOCK) void k_onehot(const int32_t* __restrict__ ids, int64_t count, int na,
+                                                   uint8_t* out)
+{
+    const int64_t i = (int64_t)blockIdx.x * TBLOCK + threadIdx.x;
+    if (i >= count * na) return;
+    const int64_t r = i / na;
+    out[i] = ids[r] == (int32_t)(i - r * na) ? 1 : 0;
+}
+
+hipError_t launch_onehot(const int32_t* ids, int64_t count, int32_t na, uint8_t* out, hipStream_t s)
+{
+    const int64_t total = count * na;
+    hipLaunchKernelGGL(k_onehot, dim3((unsigned)((total + TBLOCK - 1) / TBLOCK)), dim3(TBLOCK), 0, s, ids, count, na,
+                       out);
+    return hipGetLastError();
+}
+
+}  // namespace cs

@@ -132,20 +132,68 @@ class VecEnv:
                        'cs_observe')
         return o
 
-    def new_traj_out(self, T):
+    def new_traj_out(self, T, final_obs=False):
         o = self.new_step_out((T,))
         o['action'] = torch.empty((T, self.num_envs), dtype=self.action_dtype, device=self.device)
+        if final_obs:   # every player's observation where a game ended (Env.run's final states)
+            o['final_obs'] = torch.zeros((T, self.num_envs, self.num_players, self.obs_dim), dtype=torch.uint8,
+                                         device=self.device)
         return o
 
-    def rollout(self, T, policy_seed=0, t0=0, out=None):
-        """T lockstep steps of the uniform-random legal policy, auto-reset; -> trajectory dict of [T, N, ...]."""
-        o = out if out is not None else self.new_traj_out(T)
+    def rollout(self, T, policy_seed=0, t0=0, out=None, final_obs=False):
+        """T lockstep steps of the uniform-random legal policy, auto-reset; -> trajectory dict of [T, N, ...]
+        (+ 'final_obs' [T, N, P, obs_dim] where a game ended, when asked for or present in `out`)."""
+        o = out if out is not None else self.new_traj_out(T, final_obs)
         s = _abi.TrajOut(_ptr(o['obs']), _ptr(o['legal']), _ptr(o['player']), _ptr(o['action']),
-                         _ptr(o['reward']), _ptr(o['done']))
+                         _ptr(o['reward']), _ptr(o['done']), _ptr(o.get('final_obs')))
         with torch.cuda.device(self.device):
             _abi.check(_abi.lib().cs_rollout(self._h, int(T), int(policy_seed) & (2 ** 64 - 1), int(t0),
                                              self.env_base, C.byref(s), self._stream()), 'cs_rollout')
         return o
+
+    # -- after the rollout (SURVEY 8(f)) ----------------------------------------------------------------------------
+    def transitions(self, traj):
+        """rlcard's reorganize + DMC return target of a rollout trajectory (include/cardsim.h cs_transitions):
+        dict of [T, N] tensors next_t, end_t (int32), reward, ret (float32), done (uint8)."""
+        T = traj['player'].shape[0]
+        d = self.device
+        o = dict(next_t=torch.empty((T, self.num_envs), dtype=torch.int32, device=d),
+                 end_t=torch.empty((T, self.num_envs), dtype=torch.int32, device=d),
+                 reward=torch.empty((T, self.num_envs), dtype=torch.float32, device=d),
+                 done=torch.empty((T, self.num_envs), dtype=torch.uint8, device=d),
+                 ret=torch.empty((T, self.num_envs), dtype=torch.float32, device=d))
+        tr = _abi.TrajOut(None, None, _ptr(traj['player']), None, _ptr(traj['reward']), _ptr(traj['done']), None)
+        so = _abi.TransOut(*(_ptr(o[k]) for k in ('next_t', 'end_t', 'reward', 'done', 'ret')))
+        with torch.cuda.device(self.device):
+            _abi.check(_abi.lib().cs_transitions(self._h, int(T), C.byref(tr), C.byref(so), self._stream()),
+                       'cs_transitions')
+        return o
+
+    def legal_lists(self, legal):
+        """Bitmask rows [..., legal_bytes] -> (counts int32 [R], offsets int64 [R+1], ids int32 [total]): every row's
+        legal action ids, ascending (the keys of state['legal_actions'])."""
+        rows = legal.reshape(-1, self.legal_bytes).contiguous()
+        R = rows.shape[0]
+        counts = torch.empty(R, dtype=torch.int32, device=self.device)
+        offsets = torch.empty(R + 1, dtype=torch.int64, device=self.device)
+        L, st = _abi.lib(), self._stream()
+        with torch.cuda.device(self.device):
+            _abi.check(L.cs_legal_lists(self._h, _ptr(rows), R, _ptr(counts), _ptr(offsets), None, st), 'cs_legal_lists')
+            total = int(offsets[-1].item())
+            ids = torch.empty(max(total, 1), dtype=torch.int32, device=self.device)
+            _abi.check(L.cs_legal_lists(self._h, _ptr(rows), R, _ptr(counts), _ptr(offsets), _ptr(ids), st),
+                       'cs_legal_lists')
+        return counts, offsets, ids[:total]
+
+    def action_features(self, ids):
+        """Env.get_action_feature for a tensor of action ids -> uint8 [len(ids), action_feature_dim]."""
+        ids = torch.as_tensor(ids, device=self.device).to(torch.int32).contiguous().reshape(-1)
+        out = torch.empty((ids.numel(), self.info.action_feature_dim), dtype=torch.uint8, device=self.device)
+        if ids.numel():
+            with torch.cuda.device(self.device):
+                _abi.check(_abi.lib().cs_action_features(self._h, _ptr(ids), ids.numel(), _ptr(out), self._stream()),
+                           'cs_action_features')
+        return out
 
     # -- introspection (synchronous) ------------------------------------------------------------------------------
     def env_state_words(self, env):

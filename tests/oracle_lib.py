@@ -61,7 +61,7 @@ def lib():
         L.or_batch_reset.argtypes = [C.c_void_p] + [C.c_void_p] * 5
         L.or_batch_step.argtypes = [C.c_void_p] + [C.c_void_p] * 6
         L.or_batch_observe.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p]
-        L.or_batch_rollout.argtypes = [C.c_void_p, C.c_int32, C.c_uint64, C.c_uint64, C.c_uint64] + [C.c_void_p] * 6
+        L.or_batch_rollout.argtypes = [C.c_void_p, C.c_int32, C.c_uint64, C.c_uint64, C.c_uint64] + [C.c_void_p] * 7
         L.or_batch_draws.argtypes = [C.c_void_p, C.c_int64]
         L.or_batch_draws.restype = C.c_uint64
         L.or_holdem_rank7.argtypes = [C.c_void_p]
@@ -130,11 +130,14 @@ class Batch:
         lib().or_batch_observe(self.h, env, player, P(obs), P(legal))
         return obs, legal
 
-    def rollout(self, T, policy_seed, t0=0, env_base=0):
+    def rollout(self, T, policy_seed, t0=0, env_base=0, final_obs=False):
         o = self._out((T,))
         o['action'] = np.zeros((T, self.n), np.int32)
+        fo = None
+        if final_obs:
+            o['final_obs'] = fo = np.zeros((T, self.n, self.info.num_players, self.info.obs_dim), np.uint8)
         lib().or_batch_rollout(self.h, T, policy_seed, t0, env_base, P(o['obs']), P(o['legal']), P(o['player']),
-                               P(o['action']), P(o['reward']), P(o['done']))
+                               P(o['action']), P(o['reward']), P(o['done']), P(fo) if fo is not None else None)
         return o
 
     def draws(self, env):

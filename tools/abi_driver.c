@@ -64,6 +64,7 @@ int main(int argc, char** argv)
     for (int k = 0; k < 6; k++)
         if (hipMalloc(&dev[k], sz[k]) != hipSuccess) return 3;
     o.obs = dev[0]; o.legal = dev[1]; o.player = dev[2]; o.action = dev[3]; o.reward = dev[4]; o.done = dev[5];
+    o.final_obs = NULL;
     cs_step_out so;
     memset(&so, 0, sizeof(so));
     CHECK(cs_reset(h, &so, NULL));
@@ -95,7 +96,7 @@ int main(int argc, char** argv)
     float* tmp_r = calloc(W * info.num_players, 4);
     uint8_t* tmp_d = calloc(W, 1);
     or_batch_reset(b, tmp_o, tmp_l, tmp_p, tmp_r, tmp_d);
-    or_batch_rollout(b, T, 5, 0, 0, eo, el, ep, ea, er, ed);
+    or_batch_rollout(b, T, 5, 0, 0, eo, el, ep, ea, er, ed, NULL);
     long long bad = 0;
     for (int t = 0; t < T; t++)
         for (long long i = 0; i < W; i++) {
