@@ -19,7 +19,7 @@ constexpr int MAXP = 4;
 //   end_t   row where this row's game ends, -1 = past the window
 //   reward  the player's payoff on its last transition of the game, else 0 (reorganize: payoffs[player], done True)
 //   done    1 on that last transition
-//   ret     the player's payoff of the game (the DMC target for every step it took), NaN if the game ends past the window
+//   ret     the player's payoff of the game (the DMC target for every step it took); NaN if it ends past the window
 __global__ __launch_bounds__(TBLOCK) void k_transitions(const uint8_t* __restrict__ player,
                                                         const uint8_t* __restrict__ done,
                                                         const float* __restrict__ reward, int T, int64_t n, int P,
@@ -93,8 +93,32 @@ __global__ __launch_bounds__(TBLOCK) void k_legal_fill_small(const uint8_t* __re
     }
 }
 
-// long rows (doudizhu: 3 434 bytes): one wave per row, lane l owns a contiguous slice of the row's bytes so the
-// ids come out ascending after a wave prefix scan of the per-lane counts
+// long rows (doudizhu: 3 434 bytes): one wave per row, read as the 16-B aligned chunks that cover it (lane q takes
+// chunk q of a 64-chunk round: every load instruction moves 1 KB contiguous); bytes of the neighbouring rows are masked
+// off, and the chunk that would run past the row's end is read bytewise (it may be the buffer's end). The fill pass
+// turns each round's popcounts into write positions with a wave prefix scan, so the ids come out ascending.
+__device__ __forceinline__ uint4 row_chunk(uintptr_t cs, uintptr_t a, uintptr_t e)
+{
+    uint4 v;
+    if (cs + 16 <= e) {
+        v = *(const uint4*)cs;
+    } else {
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        for (int k = 0; k < 16 && cs + k < e; k++) w[k >> 2] |= (uint32_t)(*(const uint8_t*)(cs + k)) << (8 * (k & 3));
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    if (cs < a) {   // first chunk: drop the previous row's bytes
+        const int h = (int)(a - cs);
+        uint32_t* w = (uint32_t*)&v;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int lo = 4 * k;
+            w[k] &= lo + 4 <= h ? 0u : (lo >= h ? 0xFFFFFFFFu : (0xFFFFFFFFu << (8 * (h - lo))));
+        }
+    }
+    return v;
+}
+
 template <bool FILL>
 __global__ __launch_bounds__(TBLOCK) void k_legal_wave(const uint8_t* __restrict__ legal, int64_t rows, int lb,
                                                        int32_t* counts, const int64_t* __restrict__ offsets,
@@ -103,26 +127,42 @@ __global__ __launch_bounds__(TBLOCK) void k_legal_wave(const uint8_t* __restrict
     const int lane = threadIdx.x & (WAVE - 1);
     const int64_t r = (int64_t)blockIdx.x * (TBLOCK / WAVE) + threadIdx.x / WAVE;
     if (r >= rows) return;
-    const uint8_t* row = legal + r * lb;
-    const int per = (lb + WAVE - 1) / WAVE, k0 = lane * per, k1 = k0 + per < lb ? k0 + per : lb;
-    int c = 0;
-    for (int k = k0; k < k1; k++) c += __popc(row[k]);
+    const uintptr_t a = (uintptr_t)(legal + r * lb), a0 = a & ~(uintptr_t)15, e = a + (uintptr_t)lb;
+    const int nq = (int)((e - a0 + 15) >> 4);
     if constexpr (!FILL) {
+        int c = 0;
+        for (int q = lane; q < nq; q += WAVE) {
+            const uint4 v = row_chunk(a0 + 16 * (uintptr_t)q, a, e);
+            c += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+        }
         for (int o = WAVE / 2; o; o >>= 1) c += __shfl_xor(c, o);
         if (lane == 0) counts[r] = c;
     } else {
-        int inc = c;
-        for (int o = 1; o < WAVE; o <<= 1) {
-            const int y = __shfl_up(inc, o);
-            if (lane >= o) inc += y;
-        }
-        int64_t w = offsets[r] + (inc - c);
-        for (int k = k0; k < k1; k++) {
-            uint32_t b = row[k];
-            while (b) {
-                ids[w++] = 8 * k + __builtin_ctz(b);
-                b &= b - 1;
+        int64_t base = offsets[r];
+        for (int q0 = 0; q0 < nq; q0 += WAVE) {
+            const int q = q0 + lane;
+            const uintptr_t cs = a0 + 16 * (uintptr_t)q;
+            const uint4 v = q < nq ? row_chunk(cs, a, e) : make_uint4(0, 0, 0, 0);
+            const int c = __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+            if (!__ballot(c != 0)) continue;   // legal ids are sparse in a 27 472-bit row: most rounds are empty
+            int inc = c;
+#pragma unroll
+            for (int o = 1; o < WAVE; o <<= 1) {
+                const int y = __shfl_up(inc, o);
+                if (lane >= o) inc += y;
             }
+            int64_t w = base + (inc - c);
+            const int bit0 = 8 * (int)((intptr_t)cs - (intptr_t)a);   // id of the chunk's first bit (may be < 0)
+            const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                uint32_t b = ws[k];
+                while (b) {
+                    ids[w++] = bit0 + 32 * k + __builtin_ctz(b);
+                    b &= b - 1;
+                }
+            }
+            base += __shfl(inc, WAVE - 1);
         }
     }
 }
