@@ -110,10 +110,10 @@ void or_mt_shuffle_kat(const uint32_t *key, int key_len, const int *ns, int coun
 
 /* ---- Philox4x32-10 (Salmon et al., SC'11), the policy RNG of cs_rollout ------------------------------------------
  * counter = (env lo, env hi, t lo, t hi), key = (seed lo, seed hi); the first output word is used. */
-uint32_t or_philox_u32(uint64_t seed, uint64_t env, uint64_t t)
+/* Philox4x32-10 (Salmon et al., SC'11; Random123 round and key schedule): ctr (c0..c3), key (k0, k1) -> out[4] */
+void or_philox4(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4])
 {
-    uint32_t c0 = (uint32_t)env, c1 = (uint32_t)(env >> 32), c2 = (uint32_t)t, c3 = (uint32_t)(t >> 32);
-    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3], k0 = key[0], k1 = key[1];
     for (int r = 0; r < 10; r++) {
         uint64_t p0 = (uint64_t)0xD2511F53u * c0;
         uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
@@ -125,7 +125,19 @@ uint32_t or_philox_u32(uint64_t seed, uint64_t env, uint64_t t)
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }
-    return c0;
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* The policy's u32 for (env, step t): word t mod 4 of Philox4x32-10 keyed by the policy seed on the counter
+ * (env, t / 4) -- one Philox block serves four consecutive steps of an env. */
+uint32_t or_philox_u32(uint64_t seed, uint64_t env, uint64_t t)
+{
+    const uint64_t blk = t >> 2;
+    const uint32_t ctr[4] = {(uint32_t)env, (uint32_t)(env >> 32), (uint32_t)blk, (uint32_t)(blk >> 32)};
+    const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t out[4];
+    or_philox4(ctr, key, out);
+    return out[t & 3];
 }
 
 /* uniform over the set bits: k = floor(r * count / 2^32), then the k-th set bit in ascending action order */

@@ -36,6 +36,8 @@ void or_mt_fill(const uint32_t *key, int key_len, uint32_t *out, int n);       /
 void or_mt_shuffle_kat(const uint32_t *key, int key_len, const int *ns, int count, int16_t *out, int stride);
 
 /* ---- counter-based policy RNG (Philox4x32-10) and the uniform-legal policy of cs_rollout ------------------------ */
+void or_philox4(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+/* policy u32 of (env, step t): word t % 4 of Philox4x32-10(key = seed, counter = (env, t / 4)) */
 uint32_t or_philox_u32(uint64_t seed, uint64_t env, uint64_t t);
 int or_policy_pick(uint64_t seed, uint64_t env, uint64_t t, const uint8_t *legal_bits, int num_actions);
 

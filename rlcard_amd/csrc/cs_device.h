@@ -114,6 +114,7 @@ enum { STAGE_NONE = 0, STAGE_LDS = 2 };
 
 template <int MODE = STAGE_NONE>
 struct MtLaneT {
+    static constexpr int kMode = MODE;
     uint32_t* base;  // mt + env * MT_WORDS
     uint32_t pos;
     uint32_t stale;
@@ -407,9 +408,9 @@ __device__ __forceinline__ void stage_rows_copy(uint8_t* area, uint8_t* hbm_rows
 }
 
 // ---- Philox4x32-10 policy RNG: counter (env, t), key = policy seed. Identical to oracle/or_rng.c. ---------------
-__device__ __forceinline__ uint32_t philox_u32(uint64_t seed, uint64_t env, uint64_t t)
+__device__ __forceinline__ void philox4(uint64_t seed, uint64_t env, uint64_t blk, uint32_t (&out)[4])
 {
-    uint32_t c0 = (uint32_t)env, c1 = (uint32_t)(env >> 32), c2 = (uint32_t)t, c3 = (uint32_t)(t >> 32);
+    uint32_t c0 = (uint32_t)env, c1 = (uint32_t)(env >> 32), c2 = (uint32_t)blk, c3 = (uint32_t)(blk >> 32);
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #pragma unroll
     for (int r = 0; r < 10; r++) {
@@ -423,8 +424,36 @@ __device__ __forceinline__ uint32_t philox_u32(uint64_t seed, uint64_t env, uint
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }
-    return c0;
+    out[0] = c0;
+    out[1] = c1;
+    out[2] = c2;
+    out[3] = c3;
 }
+
+// The policy's u32 for (env, step t): word t % 4 of Philox4x32-10(key = seed, counter = (env, t / 4)), so one block
+// serves four consecutive steps (PolicyRng keeps it in registers across steps). Identical to oracle/or_rng.c.
+__device__ __forceinline__ uint32_t philox_u32(uint64_t seed, uint64_t env, uint64_t t)
+{
+    uint32_t w[4];
+    philox4(seed, env, t >> 2, w);
+    const uint32_t q = (uint32_t)t & 3u;
+    return q == 0 ? w[0] : (q == 1 ? w[1] : (q == 2 ? w[2] : w[3]));
+}
+
+struct PolicyRng {
+    uint32_t w0, w1, w2, w3;
+    // the u32 of absolute step t; steps are visited in order, a new block every fourth one
+    __device__ __forceinline__ uint32_t at(uint64_t seed, uint64_t env, uint64_t t, bool first)
+    {
+        const uint32_t q = (uint32_t)t & 3u;
+        if (first || q == 0) {
+            uint32_t w[4];
+            philox4(seed, env, t >> 2, w);
+            w0 = w[0]; w1 = w[1]; w2 = w[2]; w3 = w[3];
+        }
+        return q == 0 ? w0 : (q == 1 ? w1 : (q == 2 ? w2 : w3));
+    }
+};
 
 // uniform pick among the set bits of a <= 64-action legal mask (k = floor(r * count / 2^32), k-th set bit)
 __device__ __forceinline__ int pick_legal(uint64_t legal, uint32_t r)

@@ -313,7 +313,7 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n
 }
 
 template <class G>
-__global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n, int T,
+__global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n, int T,
                                                     uint64_t seed, uint64_t t0, uint64_t env_base, cs_traj_out out,
                                                     int flags, GameParams prm, uint32_t* sctl, uint8_t* sbuf)
 {
@@ -354,6 +354,7 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, 
     float* reward = (float*)out.reward;
     uint8_t* done_o = (uint8_t*)out.done;
     const uint64_t genv = env_base + (uint64_t)c.env;
+    PolicyRng pol;
     for (int t = 0; t < T; t++) {
 
         const int64_t rowbase = (int64_t)t * n;
@@ -361,7 +362,7 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, 
         const uint64_t lg = g.legal();
         uint32_t bits[G::NB];
         g.observe(p, bits);
-        const int a = pick_legal(lg, philox_u32(seed, genv, t0 + (uint64_t)t));
+        const int a = pick_legal(lg, pol.at(seed, genv, t0 + (uint64_t)t, t == 0));
         emit_obs<G>(lds[c.wid], bits, obs, rowbase + c.wave_first, flags, c);
         float r[G::P];
 #pragma unroll

@@ -21,6 +21,12 @@
 #ifndef CS_LEDUC_REFILL_K
 #define CS_LEDUC_REFILL_K 1
 #endif
+#ifndef CS_LEDUC_RESET_SCAN
+#define CS_LEDUC_RESET_SCAN 1
+#endif
+#ifndef CS_LEDUC_MIN_WAVES
+#define CS_LEDUC_MIN_WAVES 6
+#endif
 #ifndef CS_LEDUC_STAGE_R
 
 #define CS_LEDUC_STAGE_R 12
@@ -36,6 +42,7 @@ struct Leduc {
     // MT staging (see MtLaneT)
     static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 64, STAGE_PAD = 4, STAGE_R = CS_LEDUC_STAGE_R;
     static constexpr int RESTAGE_B = CS_LEDUC_RESTAGE_B;  // lanes restaged per pass (loads in flight): 4 > 8 > 1
+    static constexpr int MIN_WAVES = CS_LEDUC_MIN_WAVES;  // rollout waves per SIMD the register budget must allow
     static constexpr int REFILL_K = CS_LEDUC_REFILL_K;    // 1: refills are rare here, and K = 2 costs 12 VGPRs = 1 wave/SIMD
     __device__ __forceinline__ void bind(uint32_t*, const GameParams&) {}
     enum { CALL = 0, RAISE = 1, FOLD = 2, CHECK = 3 };
@@ -81,18 +88,44 @@ struct Leduc {
         set_bit(bits, in0 + in1 - my + 21);
     }
 
+    // dealer.py shuffle (intervals 5..1, swap) then randint(0, 2) for the small blind: six random_interval draws as
+    // one state machine over the draw bytes (stage q: 0..4 = the swaps, 5 = the blind), so a wave steps every lane
+    // through the staged bytes together instead of looping per interval until its slowest lane accepts
     template <class Rng>
     __device__ __forceinline__ void reset(Rng& rng)
     {
         uint32_t deck = 0x543210u;  // nibble i = card at deck position i
+        uint32_t q = 0, s = 0;
+        auto take = [&](uint32_t b) {
+            const uint32_t mx = q < 5 ? 5 - q : 1;
+            const uint32_t u = b & (mx >= 4 ? 7u : (mx >= 2 ? 3u : 1u));
+            if (u <= mx) {
+                if (q < 5) {
+                    const uint32_t ci = (deck >> (4 * mx)) & 15u, cj = (deck >> (4 * u)) & 15u, x = ci ^ cj;
+                    deck ^= (x << (4 * mx)) | (x << (4 * u));
+                } else {
+                    s = u;
+                }
+                q++;
+            }
+        };
+        if constexpr (Rng::kMode == STAGE_LDS && CS_LEDUC_RESET_SCAN) {
+            const uint32_t k0 = rng.staged_offset();
+            uint32_t k = k0;
+            while (q < 6 && k < rng.sn) {
+                const uint32_t sh = k & 3u;
+                const uint32_t w = *(const uint32_t*)(rng.stg + (k - sh)) >> (8 * sh);
 #pragma unroll
-        for (int i = 5; i >= 1; i--) {
-            const uint32_t j = rng.interval((uint32_t)i);
-            const uint32_t ci = (deck >> (4 * i)) & 15u, cj = (deck >> (4 * j)) & 15u, x = ci ^ cj;
-            deck ^= (x << (4 * i)) | (x << (4 * j));
+                for (uint32_t t = 0; t < 4; t++)
+                    if (t < 4 - sh && q < 6 && k < rng.sn) {
+                        take((w >> (8 * t)) & 255u);
+                        k++;
+                    }
+            }
+            rng.advance_by(k - k0);
         }
+        while (q < 6) take(rng.next8());
         h0 = (deck >> 20) & 15; h1 = (deck >> 16) & 15; pub = (deck >> 12) & 15;
-        const int s = (int)rng.interval(1u);
         in0 = s == 0 ? 1 : 2;
         in1 = s == 0 ? 2 : 1;
         ptr = s;

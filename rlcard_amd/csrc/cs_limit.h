@@ -104,6 +104,7 @@ struct Limit {
     // MT staging (see MtLaneT)
     static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_PAD = 8, STAGE_R = 100;
     static constexpr int RESTAGE_B = 8;  // lanes restaged per pass (loads in flight), measured: 8 > 4 > 1
+    static constexpr int MIN_WAVES = 1;  // LDS bounds the occupancy anyway
     static constexpr int REFILL_K = 2;   // stale blocks twisted per pass (see mt_refill_wave)
     __device__ __forceinline__ void bind(uint32_t*, const GameParams&) {}
     enum { CALL = 0, RAISE = 1, FOLD = 2, CHECK = 3 };
