@@ -149,6 +149,11 @@ int cs_action_features(cs_handle* h, const int32_t* ids, int64_t count, void* fe
  * Env.get_state()['raw_obs'] / get_perfect_information for single-env compatibility and debugging. Synchronous. */
 int cs_get_env_state(cs_handle* h, int64_t env, uint32_t* host_words, int32_t nwords);
 
+/* Overwrite the packed state words of env `env` from a HOST buffer taken by cs_get_env_state: Env.step_back
+ * (envs/env.py:88-108) restores the game from its history. The env's RNG stream is left where it is, as the
+ * reference's np_random is not part of the restored history. Synchronous. */
+int cs_set_env_state(cs_handle* h, int64_t env, const uint32_t* host_words, int32_t nwords);
+
 /* Stream position (u32 draws consumed) bookkeeping word of env `env` (HOST out). Synchronous; for parity tests. */
 int cs_get_rng_ctl(cs_handle* h, int64_t env, uint32_t* host_ctl);
 

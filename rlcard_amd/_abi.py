@@ -41,7 +41,8 @@ class TransOut(C.Structure):
 
 # every symbol include/cardsim.h declares (tests check the library exports all of them)
 SYMBOLS = ('cs_game_info_get', 'cs_create', 'cs_destroy', 'cs_seed', 'cs_reset', 'cs_step', 'cs_observe',
-           'cs_rollout', 'cs_transitions', 'cs_legal_lists', 'cs_action_features', 'cs_get_env_state', 'cs_get_rng_ctl', 'cs_debug_set_serial_refill', 'cs_debug_set_kernel_flags',
+           'cs_rollout', 'cs_transitions', 'cs_legal_lists', 'cs_action_features', 'cs_get_env_state',
+           'cs_set_env_state', 'cs_get_rng_ctl', 'cs_debug_set_serial_refill', 'cs_debug_set_kernel_flags',
            'cs_last_error', 'cs_version')
 
 _lib = None
@@ -73,14 +74,15 @@ def lib():
     L.cs_legal_lists.argtypes = [vp, vp, i64, vp, vp, vp, vp]
     L.cs_action_features.argtypes = [vp, vp, i64, vp, vp]
     L.cs_get_env_state.argtypes = [vp, i64, vp, i32]
+    L.cs_set_env_state.argtypes = [vp, i64, vp, i32]
     L.cs_get_rng_ctl.argtypes = [vp, i64, vp]
     L.cs_debug_set_serial_refill.argtypes = [vp, i32]
     L.cs_debug_set_kernel_flags.argtypes = [vp, i32]
     L.cs_last_error.restype = C.c_char_p
     L.cs_version.restype = C.c_char_p
-    for name in ('cs_game_info_get', 'cs_create', 'cs_seed', 'cs_reset', 'cs_step', 'cs_observe', 'cs_rollout',
-                 'cs_transitions', 'cs_legal_lists', 'cs_action_features', 'cs_get_env_state', 'cs_get_rng_ctl', 'cs_debug_set_serial_refill', 'cs_debug_set_kernel_flags'):
-        getattr(L, name).restype = C.c_int
+    for name in SYMBOLS:
+        if name not in ('cs_destroy', 'cs_last_error', 'cs_version'):
+            getattr(L, name).restype = C.c_int
     _lib = L
     return L
 

@@ -256,6 +256,25 @@ int cs_get_env_state(cs_handle* h, int64_t env, uint32_t* host_words, int32_t nw
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_get_env_state");
 }
 
+int cs_set_env_state(cs_handle* h, int64_t env, const uint32_t* host_words, int32_t nwords)
+{
+    if (!h || !host_words) return fail(CS_E_INVALID, "null argument");
+    if (env < 0 || env >= h->b.n || nwords < h->info.state_words) return fail(CS_E_INVALID, "bad env or nwords");
+    int r = set_device(h);
+    if (r != CS_OK) return r;
+    hipError_t e = hipDeviceSynchronize();
+    const int sw = h->info.state_words;
+    if (cs::state_env_major(h->b.game)) {
+        if (e == hipSuccess)
+            e = hipMemcpy(h->b.state + (size_t)env * sw, host_words, sizeof(uint32_t) * sw, hipMemcpyHostToDevice);
+    } else {
+        for (int w = 0; w < sw && e == hipSuccess; w++)
+            e = hipMemcpy(h->b.state + (size_t)w * h->b.n + env, host_words + w, sizeof(uint32_t),
+                          hipMemcpyHostToDevice);
+    }
+    return e == hipSuccess ? CS_OK : fail_hip(e, "cs_set_env_state");
+}
+
 int cs_get_rng_ctl(cs_handle* h, int64_t env, uint32_t* host_ctl)
 {
     if (!h || !host_ctl) return fail(CS_E_INVALID, "null argument");

@@ -37,6 +37,7 @@ class Env(object):
         self.timestep = 0
         self._last = None
         self._payoffs = None
+        self._history = []   # step_back: (packed state words, last outputs, payoffs) before every step
         self.seed(config.get('seed'))
 
     # -- rlcard Env API ----------------------------------------------------------------------------------------
@@ -44,6 +45,7 @@ class Env(object):
         out = self._host(self._vec.reset())
         self.action_recorder = []
         self._payoffs = None
+        self._history = []
         self._last = out
         return self._extract_state(out, out['player']), out['player']
 
@@ -54,6 +56,8 @@ class Env(object):
         if not 0 <= a < self.num_actions:
             raise ValueError('action id %d out of range [0, %d)' % (a, self.num_actions))
         decoded = self._decode_action(a)
+        if self.allow_step_back:
+            self._history.append((self._state_words(), dict(self._last), self._payoffs))
         self.timestep += 1
         self.action_recorder.append((self.get_player_id(), decoded))
         out = self._host(self._vec.step(np.array([self._action_id(decoded)], dtype=np.int32)))
@@ -63,10 +67,18 @@ class Env(object):
         return self._extract_state(out, out['player']), out['player']
 
     def step_back(self):
-        # Leduc/Limit CFR tree walking (game.py step_back) is not part of the lockstep engine
+        """env.py:88-108: restore the game as it was before the last step (the packed state words, written back
+        with cs_set_env_state); False at the start of a game. Like the reference, whose history does not hold
+        np_random, the env's RNG stream is not rewound."""
         if not self.allow_step_back:
             raise Exception('Step back is off. To use step_back, please set allow_step_back=True in rlcard.make')
-        raise NotImplementedError('step_back is not supported by the lockstep engine')
+        if not self._history:
+            return False
+        words, last, payoffs = self._history.pop()
+        self._vec.set_env_state_words(0, words)
+        self._last, self._payoffs = last, payoffs
+        player_id = self.get_player_id()
+        return self.get_state(player_id), player_id
 
     def set_agents(self, agents):
         self.agents = agents

@@ -201,6 +201,10 @@ class VecEnv:
         _abi.check(_abi.lib().cs_get_env_state(self._h, int(env), buf, self.info.state_words), 'cs_get_env_state')
         return list(buf)
 
+    def set_env_state_words(self, env, words):
+        buf = (C.c_uint32 * self.info.state_words)(*[int(w) & 0xFFFFFFFF for w in words])
+        _abi.check(_abi.lib().cs_set_env_state(self._h, int(env), buf, self.info.state_words), 'cs_set_env_state')
+
     def rng_position(self, env):
         v = C.c_uint32()
         _abi.check(_abi.lib().cs_get_rng_ctl(self._h, int(env), C.byref(v)), 'cs_get_rng_ctl')

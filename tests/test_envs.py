@@ -121,3 +121,44 @@ def test_env_run_layout_and_types(game, name):
         for a, feat in s['legal_actions'].items():
             assert np.array_equal(feat, env.get_action_feature(a))
         assert s['raw_obs']['self'] == 1 and len(s['raw_obs']['trace']) == len(env.action_recorder)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('game,name', GAMES)
+def test_step_back_restores_the_game(game, name):
+    """Env.step_back (env.py:88-108): the state before each step comes back exactly, and for games whose steps draw
+    no cards (all but blackjack) replaying the same actions reproduces the same states."""
+    env = rlcard_amd.make(game, config={'seed': 5, 'allow_step_back': True})
+    rng = np.random.RandomState(1)
+
+    def snap(s, p):
+        return (p, s['obs'].tobytes(), tuple(s['legal_actions'].keys()))
+
+    for _ in range(4):
+        state, player = env.reset()
+        assert env.step_back() is False
+        seen, acts = [snap(state, player)], []
+        while not env.is_over() and len(acts) < 12:
+            a = int(rng.choice(list(state['legal_actions'].keys())))
+            state, player = env.step(a)
+            acts.append(a)
+            seen.append(snap(state, player))
+        k = len(acts)
+        for j in range(k, 0, -1):
+            state, player = env.step_back()
+            assert snap(state, player) == seen[j - 1] and not env.is_over()
+        assert env.step_back() is False
+        if game != 'blackjack':
+            for j, a in enumerate(acts):
+                state, player = env.step(a)
+                assert snap(state, player) == seen[j + 1]
+
+
+def test_step_back_is_off_by_default():
+    import torch as _t
+    if not _t.cuda.is_available():
+        pytest.skip('needs the GPU engine')
+    env = rlcard_amd.make('leduc-holdem', config={'seed': 1})
+    env.reset()
+    with pytest.raises(Exception):
+        env.step_back()
