@@ -34,6 +34,7 @@ struct Blackjack {
     static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_PAD = 8, STAGE_R = 100;
     static constexpr int RESTAGE_B = 8;  // lanes restaged per pass (loads in flight), measured: 8 > 4 > 1
     static constexpr int MIN_WAVES = 1;  // LDS bounds the occupancy anyway
+    static constexpr int EPW = 64;        // rollout envs per wave (lane_ctx)
     static constexpr int REFILL_K = 2;   // stale blocks twisted per pass (see mt_refill_wave)
     static constexpr int HAND_CAP = 12;
 

@@ -309,13 +309,13 @@ __device__ __forceinline__ void mt_refill_wave(M& m, int lane)
 // pad is as small as the measurements allow (steady-state A/B on MI355X: Leduc W 64 + 4 fits 6 blocks per CU and is
 // 13 % faster than W + 16; Limit W 128 + 8 fits 3 blocks per CU where + 16 fitted 2, and beats + 4 by 1.5 %). The
 // persist copies move 16 / 8 / 4 B per lane, whatever the stride allows.
-template <int W, int PAD>
+template <int W, int PAD, int ROWS = WAVE>
 struct Stage {
     static_assert(W % WAVE == 0, "LDS staging rows are filled 64 words per wave instruction");
     static_assert(PAD % 4 == 0, "rows are written as dwords");
     static constexpr int STRIDE = W + PAD;
     static constexpr int CHUNK = STRIDE % 16 == 0 ? 16 : (STRIDE % 8 == 0 ? 8 : 4);   // bytes per persist copy
-    static constexpr int BYTES = WAVE * STRIDE;
+    static constexpr int BYTES = ROWS * STRIDE;
 };
 
 __device__ __forceinline__ void wave_sync_lds()
@@ -330,12 +330,12 @@ __device__ __forceinline__ void wave_sync_lds()
 // (lanes 4q gather lanes 4q+1..3 with DPP row shifts: VALU, no LDS traffic). area = the wave's staging area (lane j's
 // row at area + j * STRIDE). All 64 lanes must call.
 template <int W, int PAD, int R, int B>
-__device__ __forceinline__ void mt_restage_wave(MtLaneT<STAGE_LDS>& m, uint8_t* area, int lane)
+__device__ __forceinline__ void mt_restage_wave(MtLaneT<STAGE_LDS>& m, uint8_t* area, int lane, bool valid)
 {
     constexpr int STRIDE = Stage<W, PAD>::STRIDE, C = W / WAVE;
     m.stg = area + lane * STRIDE;
     const uint32_t k = m.staged_offset();
-    uint64_t todo = __ballot(k >= m.sn || m.sn - k < (uint32_t)R);
+    uint64_t todo = __ballot(valid && (k >= m.sn || m.sn - k < (uint32_t)R));
     while (todo) {
         // B needy lanes per pass, all their loads issued before the first is used (a pass with fewer than B left
         // repeats its first lane: same words, same bytes, harmless)
@@ -470,13 +470,13 @@ __device__ __forceinline__ int pick_legal(uint64_t legal, uint32_t r)
 // 64*ROW-byte span. Lanes build their row as bit-planes (bit b of bits[] = byte b is 1), expand it to bytes in
 // registers, stage it through LDS (odd dword stride: conflict-free ds_write_b32), and the wave writes the span
 // with 256-B dword stores.
-template <int ROW>
+template <int ROW, int ROWS = WAVE>   // ROWS: envs (rows) per wave, lanes >= ROWS hold none
 struct RowWriter {
     static_assert(ROW % 4 == 0, "byte rows must be dword multiples");
     static constexpr int DW = ROW / 4;
-    static constexpr int LDS_WORDS = WAVE * DW;   // the LDS image IS the output span (row-major, no padding)
+    static constexpr int LDS_WORDS = ROWS * DW;   // the LDS image IS the output span (row-major, no padding)
     static constexpr int NB = (ROW + 31) / 32;
-    static constexpr int Q = (WAVE * DW) / 4;     // 16-B pieces in a full span
+    static constexpr int Q = (ROWS * DW) / 4;     // 16-B pieces in a full span
 
     __device__ static __forceinline__ uint32_t expand4(uint32_t x)
     {
@@ -489,12 +489,14 @@ struct RowWriter {
     __device__ static __forceinline__ void write(uint32_t* lds, const uint32_t (&bits)[NB], uint8_t* out_span,
                                                  int lane, int nvalid, bool wide = true)
     {
+        if (lane < ROWS) {
 #pragma unroll
-        for (int j = 0; j < DW; j++) lds[lane * DW + j] = expand4(bits[j / 8] >> (4 * (j % 8)));
+            for (int j = 0; j < DW; j++) lds[lane * DW + j] = expand4(bits[j / 8] >> (4 * (j % 8)));
+        }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (wide && nvalid == WAVE && (((uintptr_t)out_span) & 15u) == 0) {
+        if (wide && nvalid == ROWS && (((uintptr_t)out_span) & 15u) == 0) {
             uint4* o = (uint4*)out_span;
             const uint4* src = (const uint4*)lds;
 #pragma unroll

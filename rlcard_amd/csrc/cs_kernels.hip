@@ -52,16 +52,19 @@ struct LaneCtx {
     bool valid;
 };
 
+// EPW envs per wave (lanes >= EPW idle): 64 everywhere but the rollouts of games with too few envs to fill the chip
+// (Limit's 262 144 envs are 4 waves per SIMD at 64 per wave; half-full waves double that -- the step is latency-bound)
+template <int EPW = WAVE>
 __device__ __forceinline__ LaneCtx lane_ctx(int64_t n)
 {
     LaneCtx c;
     c.lane = threadIdx.x & (WAVE - 1);
     c.wid = threadIdx.x / WAVE;
-    c.env = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-    c.wave_first = c.env - c.lane;
+    c.wave_first = ((int64_t)blockIdx.x * WAVES_PER_BLOCK + c.wid) * EPW;
+    c.env = c.wave_first + c.lane;
     const int64_t left = n - c.wave_first;
-    c.nvalid = left >= WAVE ? WAVE : (int)left;
-    c.valid = c.env < n;
+    c.nvalid = left >= EPW ? EPW : (left > 0 ? (int)left : 0);
+    c.valid = c.lane < EPW && c.env < n;
     return c;
 }
 
@@ -85,7 +88,7 @@ __device__ __forceinline__ void refill(M& m, int lane, int flags)
 }
 
 // obs rows: staged + coalesced when the row is a dword multiple, per-lane bytes otherwise
-template <class G>
+template <class G, int ROWS = WAVE>
 __device__ __forceinline__ void emit_obs(uint32_t* lds, const uint32_t (&bits)[G::NB], uint8_t* obs, int64_t row0, int flags,
                                          const LaneCtx& c)
 {
@@ -96,7 +99,7 @@ __device__ __forceinline__ void emit_obs(uint32_t* lds, const uint32_t (&bits)[G
             for (int k = 0; k < G::OBS; k++) o[k] = (uint8_t)(bits[k >> 2] >> (8 * (k & 3)));
         }
     } else if constexpr (G::OBS % 4 == 0) {
-        RowWriter<G::OBS>::write(lds, bits, obs + row0 * G::OBS, c.lane, c.nvalid, !(flags & 4));
+        RowWriter<G::OBS, ROWS>::write(lds, bits, obs + row0 * G::OBS, c.lane, c.nvalid, !(flags & 4));
     } else {
         if (c.valid) {
             uint8_t* o = obs + (row0 + c.lane) * G::OBS;
@@ -141,35 +144,36 @@ __device__ __forceinline__ void emit_reward(float* reward, int64_t row, const fl
     }
 }
 
-template <int ROW, bool STAGED>
+template <int ROW, bool STAGED, int ROWS>
 struct ObsWords {
     static constexpr int value = 1;
 };
-template <int ROW>
-struct ObsWords<ROW, true> {
-    static constexpr int value = RowWriter<ROW>::LDS_WORDS;
+template <int ROW, int ROWS>
+struct ObsWords<ROW, true, ROWS> {
+    static constexpr int value = RowWriter<ROW, ROWS>::LDS_WORDS;
 };
-template <class G>
+template <class G, int ROWS = WAVE>
 struct ObsLds {
-    static constexpr int WORDS = ObsWords<G::OBS, !G::RAW_OBS && G::OBS % 4 == 0>::value;
+    static constexpr int WORDS = ObsWords<G::OBS, !G::RAW_OBS && G::OBS % 4 == 0, ROWS>::value;
 };
-template <int W, int PAD, bool LDS>
+template <int W, int PAD, int ROWS, bool LDS>
 struct StageBytesOf {
     static constexpr int value = 16;
 };
-template <int W, int PAD>
-struct StageBytesOf<W, PAD, true> {
-    static constexpr int value = Stage<W, PAD>::BYTES;
+template <int W, int PAD, int ROWS>
+struct StageBytesOf<W, PAD, ROWS, true> {
+    static constexpr int value = Stage<W, PAD, ROWS>::BYTES;
 };
 template <class G>
 struct StageBytes {
-    static constexpr int value = StageBytesOf<G::STAGE_W, G::STAGE_PAD, G::STAGE_MODE == STAGE_LDS>::value;
+    static constexpr int value = StageBytesOf<G::STAGE_W, G::STAGE_PAD, G::EPW, G::STAGE_MODE == STAGE_LDS>::value;
 };
 // restage after the refill, per the game's staging mode (see MtLaneT)
 template <class G, class M>
-__device__ __forceinline__ void restage(M& m, uint8_t* area, int lane)
+__device__ __forceinline__ void restage(M& m, uint8_t* area, int lane, bool valid)
 {
-    if constexpr (G::STAGE_MODE == STAGE_LDS) mt_restage_wave<G::STAGE_W, G::STAGE_PAD, G::STAGE_R, G::RESTAGE_B>(m, area, lane);
+    if constexpr (G::STAGE_MODE == STAGE_LDS)
+        mt_restage_wave<G::STAGE_W, G::STAGE_PAD, G::STAGE_R, G::RESTAGE_B>(m, area, lane, valid);
 }
 template <class G>
 struct Scratch {   // per-lane LDS words of games that keep state in LDS (blackjack); one word per wave otherwise
@@ -180,9 +184,10 @@ __device__ __forceinline__ uint32_t* scratch_of(uint32_t* wave_area, int lane)
 {
     return G::SCRATCH_WORDS > 0 ? wave_area + lane : nullptr;
 }
-#define CS_SMEM(G)                                                  \
-    __shared__ uint32_t lds[WAVES_PER_BLOCK][ObsLds<G>::WORDS];     \
+#define CS_SMEM_ROWS(G, ROWS)                                         \
+    __shared__ uint32_t lds[WAVES_PER_BLOCK][ObsLds<G, ROWS>::WORDS]; \
     __shared__ uint32_t scr[WAVES_PER_BLOCK][Scratch<G>::WORDS]
+#define CS_SMEM(G) CS_SMEM_ROWS(G, WAVE)
 
 // ------------------------------------------------------------------------------------------------------------------
 template <class G>
@@ -317,9 +322,9 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
                                                     uint64_t seed, uint64_t t0, uint64_t env_base, cs_traj_out out,
                                                     int flags, GameParams prm, uint32_t* sctl, uint8_t* sbuf)
 {
-    CS_SMEM(G);
+    CS_SMEM_ROWS(G, G::EPW);
     __shared__ __attribute__((aligned(16))) uint8_t stage[WAVES_PER_BLOCK][StageBytes<G>::value];
-    const LaneCtx c = lane_ctx(n);
+    const LaneCtx c = lane_ctx<G::EPW>(n);
     MtLaneT<G::STAGE_MODE> m = mt_lane<G::STAGE_MODE>(mt, ctl, c);
     // MT staging needs both blocks valid at every restage, i.e. the cooperative refill (flag bit 0 off);
     // flag bit 1 disables it (one global load per draw) for A/B runs and fallback-path tests
@@ -347,7 +352,7 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
         if (g.is_over()) g.reset(m);
     }
     refill<G>(m, c.lane, flags & 1);
-    if (staged) restage<G>(m, stage[c.wid], c.lane);
+    if (staged) restage<G>(m, stage[c.wid], c.lane, c.valid);
     uint8_t* obs = (uint8_t*)out.obs;
     uint8_t* legal = (uint8_t*)out.legal;
     uint8_t* player = (uint8_t*)out.player;
@@ -363,7 +368,7 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
         uint32_t bits[G::NB];
         g.observe(p, bits);
         const int a = pick_legal(lg, pol.at(seed, genv, t0 + (uint64_t)t, t == 0));
-        emit_obs<G>(lds[c.wid], bits, obs, rowbase + c.wave_first, flags, c);
+        emit_obs<G, G::EPW>(lds[c.wid], bits, obs, rowbase + c.wave_first, flags, c);
         float r[G::P];
 #pragma unroll
         for (int k = 0; k < G::P; k++) r[k] = 0.f;
@@ -392,7 +397,7 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
             if (done) g.reset(m);
         }
         refill<G>(m, c.lane, flags & 1);
-        if (staged) restage<G>(m, stage[c.wid], c.lane);
+        if (staged) restage<G>(m, stage[c.wid], c.lane, c.valid);
     }
     bool keep = false;
     if constexpr (persist) {
@@ -410,7 +415,11 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
 
 // ------------------------------------------------------------------------------------------------------------------
 static inline GameParams params_of(const Buffers& b) { return GameParams{b.num_players, b.num_decks}; }
-static inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + BLOCK - 1) / BLOCK)); }
+static inline dim3 grid_for(int64_t n, int epw = WAVE)
+{
+    const int64_t per = (int64_t)WAVES_PER_BLOCK * epw;
+    return dim3((unsigned)((n + per - 1) / per));
+}
 
 template <class G>
 static hipError_t seed_g(const Buffers& b, const uint32_t* keys, const int32_t* klen, int64_t first, int64_t count,
@@ -443,7 +452,7 @@ template <class G>
 static hipError_t rollout_g(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
                             const cs_traj_out& o, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_rollout<G>, grid_for(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0,
+    hipLaunchKernelGGL(k_rollout<G>, grid_for(b.n, G::EPW), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0,
                        env_base, o, b.serial_refill, params_of(b), b.sctl, b.sbuf);
     return hipGetLastError();
 }

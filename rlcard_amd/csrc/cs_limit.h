@@ -25,6 +25,13 @@
 #pragma once
 #include "cs_device.h"
 
+#ifndef CS_LIMIT_MIN_WAVES
+#define CS_LIMIT_MIN_WAVES 4
+#endif
+#ifndef CS_LIMIT_EPW
+#define CS_LIMIT_EPW 32
+#endif
+
 namespace cs {
 
 __device__ __forceinline__ int top_bit(uint32_t m) { return 31 - __builtin_clz(m); }
@@ -104,7 +111,8 @@ struct Limit {
     // MT staging (see MtLaneT)
     static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_PAD = 8, STAGE_R = 100;
     static constexpr int RESTAGE_B = 8;  // lanes restaged per pass (loads in flight), measured: 8 > 4 > 1
-    static constexpr int MIN_WAVES = 1;  // LDS bounds the occupancy anyway
+    static constexpr int MIN_WAVES = CS_LIMIT_MIN_WAVES;  // rollout waves per SIMD the register budget must allow
+    static constexpr int EPW = CS_LIMIT_EPW;   // rollout envs per wave: 262 144 envs need half-full waves (lane_ctx)
     static constexpr int REFILL_K = 2;   // stale blocks twisted per pass (see mt_refill_wave)
     __device__ __forceinline__ void bind(uint32_t*, const GameParams&) {}
     enum { CALL = 0, RAISE = 1, FOLD = 2, CHECK = 3 };
