@@ -381,7 +381,17 @@ __device__ __forceinline__ Legal build_legal(const Env& e, const Cand& c, const 
 #pragma unroll
     for (int j = 0; j < 2 * PAIRS; j++) ds[j] = -1;
     int nf = 0;
-    for (int k = 0; k < (ND + WAVE - 1) / WAVE; k++) {
+    // chunks of 64 dwords that any passing group reaches (lane k tests chunk k): the others are skipped whole
+    bool chunk_pass = false;
+    if (lane < (ND + WAVE - 1) / WAVE) {
+        const int last = lane * WAVE + WAVE - 1 < ND ? lane * WAVE + WAVE - 1 : ND - 1;
+        const uint32_t lo = T.drange[lane * WAVE] & 0xFFFFu, hi = T.drange[last] >> 16;
+        chunk_pass = L.pre[hi + 1] > L.pre[lo];
+    }
+    uint64_t chunks = __ballot(chunk_pass);
+    while (chunks) {
+        const int k = __builtin_ctzll(chunks);
+        chunks &= chunks - 1;
         const int d = k * WAVE + lane;
         bool pass = false;
         if (d < ND) {
