@@ -89,14 +89,20 @@ __device__ __forceinline__ void mt_twist_wave(const uint32_t* __restrict__ src, 
     }
 }
 
+// Global-address-space view of a pointer into HBM: pointers rebuilt from integers (readlane) are generic, and generic
+// accesses compile to flat_load/flat_store, which count on lgkmcnt too, so every use waits with vmcnt(0) lgkmcnt(0)
+// -- draining the wave's outstanding trajectory stores each time (measured in the k_rollout ISA)
+typedef __attribute__((address_space(1))) uint32_t gu32;
+__device__ __forceinline__ gu32* to_global(uint32_t* p) { return (gu32*)p; }
+
 // 64-bit pointer held by lane j (readlane returns int: go through uint32_t so bit 31 of the low half is not
 // sign-extended into the high half)
-__device__ __forceinline__ uint32_t* lane_ptr(uint32_t* p, int j)
+__device__ __forceinline__ gu32* lane_ptr(uint32_t* p, int j)
 {
     const uint64_t b = (uint64_t)(uintptr_t)p;
     const uint64_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, j);
     const uint64_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), j);
-    return (uint32_t*)(uintptr_t)(lo | (hi << 32));
+    return (gu32*)(uintptr_t)(lo | (hi << 32));
 }
 
 // One lane's view of its env's stream. MODE selects how draws are served:
@@ -235,7 +241,7 @@ using MtLane = MtLaneT<STAGE_NONE>;
 
 // dst[s] = twist(src[s]) for K streams at once, phases interleaved so the K twists' loads overlap (see mt_twist_wave)
 template <int K>
-__device__ __forceinline__ void mt_twist_wave_k(const uint32_t* const (&src)[K], uint32_t* const (&dst)[K], int lane)
+__device__ __forceinline__ void mt_twist_wave_k(const gu32* const (&src)[K], gu32* const (&dst)[K], int lane)
 {
     constexpr int H = MT_N - MT_M;  // 227
     uint32_t n1[K][4], n2[K][4];
@@ -284,15 +290,15 @@ __device__ __forceinline__ void mt_refill_wave(M& m, int lane)
 {
     uint64_t need = __ballot(m.stale != 0);
     while (need) {
-        const uint32_t* src[K];
-        uint32_t* dst[K];
+        const gu32* src[K];
+        gu32* dst[K];
         int j0 = -1;
 #pragma unroll
         for (int s = 0; s < K; s++) {
             const int j = need ? __builtin_ctzll(need) : j0;
             need &= need - 1;
             if (s == 0) j0 = j;
-            uint32_t* b = lane_ptr(m.base, j);
+            gu32* b = lane_ptr(m.base, j);
             const uint32_t c = __builtin_amdgcn_readlane(m.pos, j) < MT_N ? 0 : MT_N;
             src[s] = b + c;
             dst[s] = b + (MT_N - c);
@@ -350,7 +356,7 @@ __device__ __forceinline__ void mt_restage_wave(MtLaneT<STAGE_LDS>& m, uint8_t* 
         uint32_t ps[B], v[B][C];
 #pragma unroll
         for (int b = 0; b < B; b++) {
-            const uint32_t* jb = lane_ptr(m.base, js[b]);
+            const gu32* jb = lane_ptr(m.base, js[b]);
             ps[b] = __builtin_amdgcn_readlane(m.pos, js[b]);
 #pragma unroll
             for (int c = 0; c < C; c++) {

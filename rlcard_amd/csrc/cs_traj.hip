@@ -100,11 +100,15 @@ __global__ __launch_bounds__(TBLOCK) void k_legal_fill_small(const uint8_t* __re
 __device__ __forceinline__ uint4 row_chunk(uintptr_t cs, uintptr_t a, uintptr_t e)
 {
     uint4 v;
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) const v4u g4;   // global, not flat (see cs_device.h to_global)
+    typedef __attribute__((address_space(1))) const uint8_t g1;
     if (cs + 16 <= e) {
-        v = *(const uint4*)cs;
+        const v4u t = *(g4*)cs;
+        v = make_uint4(t.x, t.y, t.z, t.w);
     } else {
         uint32_t w[4] = {0u, 0u, 0u, 0u};
-        for (int k = 0; k < 16 && cs + k < e; k++) w[k >> 2] |= (uint32_t)(*(const uint8_t*)(cs + k)) << (8 * (k & 3));
+        for (int k = 0; k < 16 && cs + k < e; k++) w[k >> 2] |= (uint32_t)(*(g1*)(cs + k)) << (8 * (k & 3));
         v = make_uint4(w[0], w[1], w[2], w[3]);
     }
     if (cs < a) {   // first chunk: drop the previous row's bytes
