@@ -7,7 +7,7 @@ N>1: one process per GPU (torchrun), rank r owns envs [r*N, (r+1)*N) seeded 42 +
 independent, so there is no data-path collective (weak scaling); --gather adds the optional RCCL all-gather of the
 trajectory shards (timed separately, reported under "gather").
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--game leduc-holdem] [--envs N_PER_GPU] [--T 16]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--game leduc-holdem] [--envs N_PER_GPU] [--T 64]
 """
 import argparse
 import json
@@ -82,7 +82,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--game', default='leduc-holdem', choices=sorted(GAMES))
     ap.add_argument('--envs', type=int, default=0, help='envs per GPU (default: the BASELINE config)')
-    ap.add_argument('--T', type=int, default=16, help='fused env steps per launch')
+    ap.add_argument('--T', type=int, default=64, help='fused env steps per launch')
     ap.add_argument('--gather', action='store_true', help='also all-gather trajectory shards over RCCL')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-precondition', dest='precondition', action='store_false',

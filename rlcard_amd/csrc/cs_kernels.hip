@@ -368,15 +368,19 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
         uint32_t bits[G::NB];
         g.observe(p, bits);
         const int a = pick_legal(lg, pol.at(seed, genv, t0 + (uint64_t)t, t == 0));
+#ifndef CS_PROF_NO_OBS   // profiling builds only (tools: make variant DEFS=-DCS_PROF_NO_OBS): outputs incomplete
         emit_obs<G, G::EPW>(lds[c.wid], bits, obs, rowbase + c.wave_first, flags, c);
+#endif
         float r[G::P];
 #pragma unroll
         for (int k = 0; k < G::P; k++) r[k] = 0.f;
         bool done = false;
         if (c.valid) {
             const int64_t row = rowbase + c.env;
+#ifndef CS_PROF_NO_SMALL
             emit_legal<G>(legal, row, lg);
             player[row] = (uint8_t)p;
+#endif
             if constexpr (G::ACTION_BYTES == 1) ((uint8_t*)out.action)[row] = (uint8_t)a;
             else ((int16_t*)out.action)[row] = (int16_t)a;
             g.step(a, m);
@@ -392,8 +396,10 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
                     }
                 }
             }
+#ifndef CS_PROF_NO_SMALL
             emit_reward<G>(reward, row, r);
             done_o[row] = (uint8_t)done;
+#endif
             if (done) g.reset(m);
         }
         refill<G>(m, c.lane, flags & 1);
