@@ -1,13 +1,13 @@
 #!/usr/bin/env python3
 """Benchmark of the env.step hot path (BASELINE.json): env-steps/s (whole node) + achieved HBM GB/s.
 
-One bench "step" = one cs_rollout launch: T fused lockstep env steps (uniform-random legal policy, auto-reset) over
+One bench "step" = one cs_rollout launch: T fused lockstep env steps (Leduc 128, others 64 by default) (uniform-random legal policy, auto-reset) over
 every env of the rank's shard, writing the full trajectory (obs, legal mask, player, action, reward, done) to HBM.
 N>1: one process per GPU (torchrun), rank r owns envs [r*N, (r+1)*N) seeded 42 + global index -- the envs are
 independent, so there is no data-path collective (weak scaling); --gather adds the optional RCCL all-gather of the
 trajectory shards (timed separately, reported under "gather").
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--game leduc-holdem] [--envs N_PER_GPU] [--T 64]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--game leduc-holdem] [--envs N_PER_GPU] [--T STEPS]
 """
 import argparse
 import json
@@ -21,14 +21,14 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md (chip-level parameters)
 
-# per game: default envs per GPU (BASELINE.json configs), packed state bytes per env read+written once per launch
-# (state words + the RNG control word), and the expected tempered-u32 MT19937 draws per env-step under random play
-# (exact acceptance rates of random_interval x random-play game lengths).
+# per game: default envs per GPU (BASELINE.json configs), default fused steps per launch, packed state bytes per env
+# read + written once per launch (state words + the RNG control word), and the expected tempered-u32 MT19937 draws
+# per env-step under random play (exact acceptance rates of random_interval x random-play game lengths).
 GAMES = {
-    'leduc-holdem': dict(envs=1 << 20, state_bytes=2 * 4 + 4, draws_per_step=2.83),
-    'limit-holdem': dict(envs=262144, state_bytes=12 * 4 + 4, draws_per_step=24.5),
-    'blackjack': dict(envs=1 << 20, state_bytes=20 * 4 + 4, draws_per_step=57.0),
-    'doudizhu': dict(envs=65536, state_bytes=20 * 4 + 4, draws_per_step=1.21),
+    'leduc-holdem': dict(envs=1 << 20, T=128, state_bytes=2 * 4 + 4, draws_per_step=2.83),
+    'limit-holdem': dict(envs=262144, T=64, state_bytes=12 * 4 + 4, draws_per_step=24.5),
+    'blackjack': dict(envs=1 << 20, T=64, state_bytes=20 * 4 + 4, draws_per_step=57.0),
+    'doudizhu': dict(envs=65536, T=64, state_bytes=20 * 4 + 4, draws_per_step=1.21),
 }
 
 
@@ -82,7 +82,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--game', default='leduc-holdem', choices=sorted(GAMES))
     ap.add_argument('--envs', type=int, default=0, help='envs per GPU (default: the BASELINE config)')
-    ap.add_argument('--T', type=int, default=64, help='fused env steps per launch')
+    ap.add_argument('--T', type=int, default=0, help='fused env steps per launch (default: per game, GAMES)')
     ap.add_argument('--gather', action='store_true', help='also all-gather trajectory shards over RCCL')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-precondition', dest='precondition', action='store_false',
@@ -107,7 +107,8 @@ def main():
         if world > 1:
             dist.barrier()
 
-    game, T = args.game, args.T
+    game = args.game
+    T = args.T or GAMES[game]['T']   # measured: longer launches amortise the state / staging traffic
     N = args.envs or GAMES[game]['envs']
     env = ShardedVecEnv(game, N, rank, seed=42, device=local)   # global envs [rank*N, (rank+1)*N)
     env.reset()
