@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Benchmark of the env.step hot path (BASELINE.json): env-steps/s (whole node) + achieved HBM GB/s.
 
-One bench "step" = one cs_rollout launch: T fused lockstep env steps (Leduc 128, others 64 by default) (uniform-random legal policy, auto-reset) over
-every env of the rank's shard, writing the full trajectory (obs, legal mask, player, action, reward, done) to HBM.
+One bench "step" = one cs_rollout launch: T fused lockstep env steps (default Leduc 128, the others 64) of the
+uniform-random legal policy with auto-reset over every env of the rank's shard, writing the full trajectory (obs,
+legal mask, player, action, reward, done) to HBM.
 N>1: one process per GPU (torchrun), rank r owns envs [r*N, (r+1)*N) seeded 42 + global index -- the envs are
 independent, so there is no data-path collective (weak scaling); --gather adds the optional RCCL all-gather of the
 trajectory shards (timed separately, reported under "gather").
