@@ -25,8 +25,17 @@
 #pragma once
 #include "cs_device.h"
 
+#ifndef CS_LIMIT_STAGE_W
+#define CS_LIMIT_STAGE_W 128
+#endif
+#ifndef CS_LIMIT_STAGE_R
+#define CS_LIMIT_STAGE_R 100
+#endif
+#ifndef CS_LIMIT_RESTAGE_B
+#define CS_LIMIT_RESTAGE_B 8
+#endif
 #ifndef CS_LIMIT_MIN_WAVES
-#define CS_LIMIT_MIN_WAVES 4
+#define CS_LIMIT_MIN_WAVES 5
 #endif
 #ifndef CS_LIMIT_EPW
 #define CS_LIMIT_EPW 32
@@ -45,17 +54,21 @@ __device__ __forceinline__ int top_straight13(uint32_t mask)
 }
 
 // 7-card hand value; larger = better, equal = split. cat << 20 | five 4-bit tiebreak ranks
-__device__ inline uint32_t holdem_rank7(const int (&c)[7])
+// a card (card2index: suit * 13 + (A, 2..K)) into the evaluator's tallies: 13 rank-count nibbles (2 = 0 .. A = 12)
+// and a 13-bit rank mask per suit (packed 4 x 16 bits)
+__device__ __forceinline__ void tally_card(int c, uint64_t& cnt, uint64_t& sm)
 {
-    uint64_t cnt = 0;          // 13 nibbles: count per rank
-    uint32_t sm[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 7; k++) {
-        const int s = c[k] / 13, q = c[k] - 13 * s, r = q == 0 ? 12 : q - 1;
-        cnt += 1ull << (4 * r);
-        const uint32_t b = 1u << r;
-        sm[0] |= s == 0 ? b : 0u; sm[1] |= s == 1 ? b : 0u; sm[2] |= s == 2 ? b : 0u; sm[3] |= s == 3 ? b : 0u;
-    }
+    const int s = c / 13, q = c - 13 * s, r = q == 0 ? 12 : q - 1;
+    cnt += 1ull << (4 * r);
+    sm |= 1ull << (16 * s + r);
+}
+
+// 7-card category << 20 | five tiebreak ranks, from the tallies of the 7 cards (the board's are shared by both
+// players: tallied once)
+__device__ inline uint32_t holdem_rank7(uint64_t cnt, uint64_t smp)
+{
+    const uint32_t sm[4] = {(uint32_t)smp & 0x1FFFu, (uint32_t)(smp >> 16) & 0x1FFFu, (uint32_t)(smp >> 32) & 0x1FFFu,
+                            (uint32_t)(smp >> 48) & 0x1FFFu};
     uint32_t m1 = 0, m2 = 0, m3 = 0, m4 = 0;
 #pragma unroll
     for (int r = 0; r < 13; r++) {
@@ -109,9 +122,9 @@ struct Limit {
     static constexpr bool RAW_OBS = false;
     static constexpr int SCRATCH_WORDS = 0;
     // MT staging (see MtLaneT)
-    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_PAD = 8, STAGE_R = 100;
-    static constexpr int RESTAGE_B = 8;  // lanes restaged per pass (loads in flight), measured: 8 > 4 > 1
-    static constexpr int MIN_WAVES = CS_LIMIT_MIN_WAVES;  // rollout waves per SIMD the register budget must allow
+    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = CS_LIMIT_STAGE_W, STAGE_PAD = 8, STAGE_R = CS_LIMIT_STAGE_R;
+    static constexpr int RESTAGE_B = CS_LIMIT_RESTAGE_B;  // lanes restaged per pass (loads in flight)
+    static constexpr int MIN_WAVES = CS_LIMIT_MIN_WAVES;  // 5 waves/SIMD: beats 4 (no spills) and 6 (40 spilled VGPRs)
     static constexpr int EPW = CS_LIMIT_EPW;   // rollout envs per wave: 262 144 envs need half-full waves (lane_ctx)
     static constexpr int REFILL_K = 2;   // stale blocks twisted per pass (see mt_refill_wave)
     __device__ __forceinline__ void bind(uint32_t*, const GameParams&) {}
@@ -174,30 +187,34 @@ struct Limit {
     template <class Rng>
     __device__ __forceinline__ void reset(Rng& rng)
     {
-        int J[9], V[9], D[9];
+        // swap k writes card vj to position 51 - k (dealt: D[k]) and card vi to position j (JV[k] = j | vi << 8,
+        // looked up by the later swaps); D[k] goes straight into its packed field (registers: the rollout kernel's
+        // occupancy is register-bound here)
+        uint32_t JV[9];
+        uint32_t d0 = 0, d1 = 0;
 #pragma unroll
         for (int k = 0; k < 9; k++) {
-            const int i = 51 - k;
-            const int j = (int)rng.interval((uint32_t)i);
-            int vi = i, vj = j;
+            const uint32_t i = 51 - k;
+            const uint32_t j = rng.interval(i);
+            uint32_t vi = i, vj = j;
 #pragma unroll
             for (int q = 0; q < k; q++) {   // oldest -> newest: the newest write to a position wins
-                vi = J[q] == i ? V[q] : vi;
-                vj = J[q] == j ? V[q] : vj;
+                const uint32_t jq = JV[q] & 255u, vq = JV[q] >> 8;
+                vi = jq == i ? vq : vi;
+                vj = jq == j ? vq : vj;
             }
-            D[k] = vj;
-            J[k] = j;
-            V[k] = vi;
+            JV[k] = j | (vi << 8);
+            constexpr int F0[4] = {0, 12, 6, 18};   // hole i -> player i % 2, card i / 2 (w0 layout)
+            if (k < 4) d0 |= vj << F0[k < 4 ? k : 0];
+            else d1 |= vj << (6 * (k - 4));
         }
         rng.skip_intervals(42u);   // deck positions 42..1 are never dealt: only the words they consume matter
         // hole i -> player i%2, card i/2, from deck[51-i] = D[i]
         const int s = (int)rng.interval(1u);
         const int in_0 = s == 0 ? 1 : 2, in_1 = s == 0 ? 2 : 1;
         const int first = s;  // (BB + 1) % 2 with BB = (s + 1) % 2
-        w0 = (uint32_t)D[0] | (uint32_t)D[2] << 6 | (uint32_t)D[1] << 12 | (uint32_t)D[3] << 18 |
-             (uint32_t)in_0 << 24 | (uint32_t)first << 30;
-        w1 = (uint32_t)D[4] | (uint32_t)D[5] << 6 | (uint32_t)D[6] << 12 | (uint32_t)D[7] << 18 |
-             (uint32_t)D[8] << 24;
+        w0 = d0 | (uint32_t)in_0 << 24 | (uint32_t)first << 30;
+        w1 = d1;
         w2 = (uint32_t)in_1 | (uint32_t)in_0 << 6 | (uint32_t)in_1 << 11 | 1u << 26;  // raised = in_chips, use_prev
         w3 = (w3 & 0xFFFu) << 12;                                                      // prev <- current, current <- 0
     }
@@ -235,9 +252,17 @@ struct Limit {
         if (f0() || f1()) {
             win0 = !f0(); win1 = !f1();
         } else {
-            int c0[7] = {hole(0, 0), hole(0, 1), board(0), board(1), board(2), board(3), board(4)};
-            int c1[7] = {hole(1, 0), hole(1, 1), board(0), board(1), board(2), board(3), board(4)};
-            const uint32_t v0 = holdem_rank7(c0), v1 = holdem_rank7(c1);
+            uint64_t bc = 0, bs = 0;
+#pragma unroll
+            for (int k = 0; k < 5; k++) tally_card(board(k), bc, bs);
+            uint64_t c0 = bc, s0 = bs;
+            tally_card(hole(0, 0), c0, s0);
+            tally_card(hole(0, 1), c0, s0);
+            const uint32_t v0 = holdem_rank7(c0, s0);
+            uint64_t c1 = bc, s1 = bs;
+            tally_card(hole(1, 0), c1, s1);
+            tally_card(hole(1, 1), c1, s1);
+            const uint32_t v1 = holdem_rank7(c1, s1);
             win0 = v0 >= v1; win1 = v1 >= v0;
         }
         const int a = in0(), b = in1(), m = a < b ? a : b;
