@@ -30,6 +30,8 @@ GAMES = {
     'limit-holdem': dict(envs=262144, T=64, state_bytes=12 * 4 + 4, draws_per_step=24.5),
     'blackjack': dict(envs=1 << 20, T=64, state_bytes=20 * 4 + 4, draws_per_step=57.0),
     'doudizhu': dict(envs=65536, T=64, state_bytes=20 * 4 + 4, draws_per_step=1.21),
+    # not a BASELINE config; draws/step counted on the oracle (4096 envs x 256 random steps)
+    'no-limit-holdem': dict(envs=262144, T=64, state_bytes=4 * 4 + 4, draws_per_step=26.3),
 }
 
 

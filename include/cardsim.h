@@ -29,21 +29,23 @@ enum {
 };
 
 /* game ids; names as registered by rlcard/envs/__init__.py:6-54 */
-enum { CS_GAME_BLACKJACK = 0, CS_GAME_LEDUC = 1, CS_GAME_LIMIT = 2, CS_GAME_DOUDIZHU = 3 };
+enum { CS_GAME_BLACKJACK = 0, CS_GAME_LEDUC = 1, CS_GAME_LIMIT = 2, CS_GAME_DOUDIZHU = 3, CS_GAME_NOLIMIT = 4 };
 
 typedef struct cs_handle cs_handle;
 
 /* Game configuration: the 'game_*' keys Env.__init__ forwards to Game.configure (rlcard/envs/env.py:33-39). */
 typedef struct {
-    int32_t num_players; /* blackjack 'game_num_players' (default 1); leduc/limit 2; doudizhu 3 (0 = default) */
+    int32_t num_players; /* blackjack 'game_num_players' (default 1); leduc/limit/no-limit 2; doudizhu 3 (0 = default) */
     int32_t num_decks;   /* blackjack 'game_num_decks' (default 1, 0 = infinite); ignored elsewhere (-1 = default) */
-    int32_t reserved[6];
+    int32_t chips_for_each; /* no-limit 'chips_for_each' (nolimitholdem/game.py:45-56): stack, 1..255 (0 = 100) */
+    int32_t dealer_plus1;   /* no-limit 'dealer_id' + 1: 0 = None (drawn by the first game, then kept), 1..2 fixed */
+    int32_t reserved[4];
 } cs_config;
 
 /* Static shape of a game (rlcard Env.num_players / num_actions / state_shape). */
 typedef struct {
-    int32_t obs_dim;      /* bytes per obs row: leduc 36, limit 72, blackjack 2, doudizhu 901 (landlord rows use 790) */
-    int32_t num_actions;  /* leduc/limit 4, blackjack 2, doudizhu 27472 */
+    int32_t obs_dim;      /* bytes per obs row: leduc 36, limit 72, no-limit 54, blackjack 2, doudizhu 901 (landlord 790) */
+    int32_t num_actions;  /* leduc/limit 4, no-limit 5, blackjack 2, doudizhu 27472 */
     int32_t num_players;
     int32_t legal_bytes;  /* ceil(num_actions / 8): legal-action bitmask bytes per row */
     int32_t action_bytes; /* dtype width of rollout action rows: 1 (uint8) or 2 (int16, doudizhu) */
@@ -53,7 +55,8 @@ typedef struct {
 } cs_game_info;
 
 /* Outputs of reset/step/observe, all device pointers, one row per env:
- *   obs    uint8  [n][obs_dim]     the current player's observation (values 0/1; blackjack: the two scores)
+ *   obs    uint8  [n][obs_dim]     the current player's observation (values 0/1; blackjack: the two scores;
+ *                                  no-limit: 52 card bits, then my chips and the largest chips in the pot)
  *   legal  uint8  [n][legal_bytes] legal-action bitmask, bit a of byte a/8 (LSB first) = action id a
  *   player uint8  [n]              current player id (Env.get_player_id)
  *   reward float  [n][num_players] payoffs of the transition (non-zero only where done; Env.get_payoffs)

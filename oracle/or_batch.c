@@ -28,6 +28,7 @@ static const or_game_vt *vt_of(int game)
     case OR_LEDUC: return &or_leduc_vt;
     case OR_LIMIT: return &or_limit_vt;
     case OR_DOUDIZHU: return &or_doudizhu_vt;
+    case OR_NOLIMIT: return &or_nolimit_vt;
     default: return NULL;
     }
 }

@@ -19,6 +19,7 @@ extern const or_game_vt or_leduc_vt;
 extern const or_game_vt or_limit_vt;
 extern const or_game_vt or_blackjack_vt;
 extern const or_game_vt or_doudizhu_vt;
+extern const or_game_vt or_nolimit_vt;
 
 /* numpy RandomState.shuffle of an int array (Fisher-Yates, i = n-1..1, j = random_interval(i)) */
 static inline void or_shuffle_int(or_mt *rng, int *x, int n)

@@ -42,11 +42,13 @@ uint32_t or_philox_u32(uint64_t seed, uint64_t env, uint64_t t);
 int or_policy_pick(uint64_t seed, uint64_t env, uint64_t t, const uint8_t *legal_bits, int num_actions);
 
 /* ---- games ------------------------------------------------------------------------------------------------------ */
-enum { OR_BLACKJACK = 0, OR_LEDUC = 1, OR_LIMIT = 2, OR_DOUDIZHU = 3 };
+enum { OR_BLACKJACK = 0, OR_LEDUC = 1, OR_LIMIT = 2, OR_DOUDIZHU = 3, OR_NOLIMIT = 4 };
 
 typedef struct {
     int32_t num_players;  /* blackjack: game_num_players; leduc/limit: 2; doudizhu: 3 */
     int32_t num_decks;    /* blackjack only (0 = infinite) */
+    int32_t chips_for_each; /* no-limit only: stack per player (1..255) */
+    int32_t dealer_id;      /* no-limit only: -1 = drawn by the first init_game, else fixed */
 } or_cfg;
 
 typedef struct {

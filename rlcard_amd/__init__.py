@@ -1,4 +1,5 @@
-"""rlcard_amd -- MI355X-native batched card-game environments (Blackjack, Leduc Hold'em, Limit Hold'em, DouDizhu).
+"""rlcard_amd -- MI355X-native batched card-game environments (Blackjack, Leduc Hold'em, Limit Hold'em,
+No-limit Hold'em, DouDizhu).
 
 Drop-in for the reference's env path: rlcard_amd.make(env_id, config) returns an Env with rlcard's
 reset/step/run/get_state/get_payoffs API (rlcard/envs/env.py), and rlcard_amd.VecEnv runs N such envs in lockstep

@@ -8,14 +8,15 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, os.environ.get('CARDSIM_LIB', 'libcardsim.so'))   # CARDSIM_LIB: A/B builds only
 
-GAME_IDS = {'blackjack': 0, 'leduc-holdem': 1, 'limit-holdem': 2, 'doudizhu': 3}
+GAME_IDS = {'blackjack': 0, 'leduc-holdem': 1, 'limit-holdem': 2, 'doudizhu': 3, 'no-limit-holdem': 4}
 
 CS_OK = 0
 _ERRORS = {-1: 'CS_E_INVALID', -2: 'CS_E_DEVICE', -3: 'CS_E_STATE', -4: 'CS_E_UNSUPPORTED'}
 
 
 class Config(C.Structure):
-    _fields_ = [('num_players', C.c_int32), ('num_decks', C.c_int32), ('reserved', C.c_int32 * 6)]
+    _fields_ = [('num_players', C.c_int32), ('num_decks', C.c_int32), ('chips_for_each', C.c_int32),
+                ('dealer_plus1', C.c_int32), ('reserved', C.c_int32 * 4)]
 
 
 class GameInfo(C.Structure):
@@ -93,8 +94,8 @@ def check(code, what=''):
         raise CardsimError('%s failed (%s): %s' % (what, _ERRORS.get(code, code), msg))
 
 
-def game_info(game, num_players=0, num_decks=-1):
-    cfg = Config(num_players, num_decks)
+def game_info(game, num_players=0, num_decks=-1, chips_for_each=0, dealer_id=None):
+    cfg = Config(num_players, num_decks, chips_for_each, 0 if dealer_id is None else int(dealer_id) + 1)
     info = GameInfo()
     check(lib().cs_game_info_get(GAME_IDS[game] if isinstance(game, str) else game, C.byref(cfg), C.byref(info)),
           'cs_game_info_get')

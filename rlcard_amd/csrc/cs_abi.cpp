@@ -82,6 +82,8 @@ int cs_create(cs_handle** out, int32_t game, int64_t num_envs, int32_t device, c
     h->b.n = num_envs;
     h->b.num_players = info.num_players;
     h->b.num_decks = cfg ? cfg->num_decks : 1;
+    h->b.chips_for_each = (cfg && cfg->chips_for_each > 0) ? cfg->chips_for_each : 100;
+    h->b.dealer_id = cfg ? cfg->dealer_plus1 - 1 : -1;
     h->b.serial_refill = 0;
     h->b.table = nullptr;
     if ((r = set_device(h)) != CS_OK) { delete h; return r; }

@@ -23,10 +23,12 @@ constexpr int MT_WORDS = 2 * MT_N;
 constexpr uint32_t CTL_STALE = 1u << 16;
 constexpr int WAVE = 64;
 
-// runtime game configuration (cs_config): only blackjack reads it
+// runtime game configuration (cs_config): blackjack reads players / decks, no-limit hold'em stacks / dealer
 struct GameParams {
     int32_t num_players;
     int32_t num_decks;
+    int32_t chips_for_each;   // no-limit: stack per player
+    int32_t dealer_id;        // no-limit: -1 = drawn by the first reset (rlcard's None), else fixed
 };
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y)
@@ -522,6 +524,51 @@ struct RowWriter {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+};
+
+// Same span writer for rows of raw byte values (ROW even): words[] holds the row's bytes four per word (byte k in
+// byte k % 4 of words[k / 4]); lanes write their row into the LDS image as 16-bit pieces (ROW % 4 == 2) or dwords,
+// and the span leaves with 16-B stores when it is a whole, aligned number of 16-B pieces.
+template <int ROW, int ROWS = WAVE>
+struct RowWriterRaw {
+    static_assert(ROW % 2 == 0, "raw rows are staged as 16-bit pieces");
+    static constexpr int NW = (ROW + 3) / 4;
+    static constexpr int SPAN = ROWS * ROW;
+    static constexpr int LDS_WORDS = (SPAN + 3) / 4;
+
+    __device__ static __forceinline__ void write(uint32_t* lds, const uint32_t (&words)[NW], uint8_t* out_span,
+                                                 int lane, int nvalid, bool wide = true)
+    {
+        if (lane < ROWS) {
+            if constexpr (ROW % 4 == 0) {
+#pragma unroll
+                for (int j = 0; j < ROW / 4; j++) lds[lane * (ROW / 4) + j] = words[j];
+            } else {
+                uint16_t* l16 = (uint16_t*)lds + lane * (ROW / 2);
+#pragma unroll
+                for (int j = 0; j < ROW / 2; j++) l16[j] = (uint16_t)(words[j / 2] >> (16 * (j & 1)));
+            }
+        }
+        wave_sync_lds();
+        const int bytes = nvalid * ROW;
+        if (SPAN % 16 == 0 && wide && nvalid == ROWS && (((uintptr_t)out_span) & 15u) == 0) {
+            uint4* o = (uint4*)out_span;
+            const uint4* src = (const uint4*)lds;
+#pragma unroll
+            for (int j = 0; j < (SPAN / 16 + WAVE - 1) / WAVE; j++) {
+                const int q = j * WAVE + lane;
+                if (q < SPAN / 16) o[q] = src[q];
+            }
+        } else if (bytes % 4 == 0 && (((uintptr_t)out_span) & 3u) == 0) {
+            uint32_t* o = (uint32_t*)out_span;
+            for (int e = lane; e < bytes / 4; e += WAVE) o[e] = lds[e];
+        } else {
+            uint16_t* o = (uint16_t*)out_span;
+            const uint16_t* src = (const uint16_t*)lds;
+            for (int e = lane; e < bytes / 2; e += WAVE) o[e] = src[e];
+        }
+        wave_sync_lds();
     }
 };
 

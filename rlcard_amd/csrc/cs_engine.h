@@ -18,6 +18,7 @@ struct Buffers {
     uint8_t* sbuf;    // [n][stage bytes] rollout MT staging rows persisted between launches
     const void* table;  // game-specific read-only table (doudizhu action table), or null
     int32_t num_players, num_decks;
+    int32_t chips_for_each, dealer_id;   // no-limit hold'em (cs_config; dealer_id -1 = drawn)
     int32_t serial_refill;  // testing hook
 };
 

@@ -10,6 +10,7 @@
 #include "cs_limit.h"
 #include "cs_blackjack.h"
 #include "cs_doudizhu.h"
+#include "cs_nolimit.h"
 
 namespace cs {
 
@@ -92,7 +93,9 @@ template <class G, int ROWS = WAVE>
 __device__ __forceinline__ void emit_obs(uint32_t* lds, const uint32_t (&bits)[G::NB], uint8_t* obs, int64_t row0, int flags,
                                          const LaneCtx& c)
 {
-    if constexpr (G::RAW_OBS) {
+    if constexpr (G::RAW_OBS && G::OBS % 2 == 0) {
+        RowWriterRaw<G::OBS, ROWS>::write(lds, bits, obs + row0 * G::OBS, c.lane, c.nvalid, !(flags & 4));
+    } else if constexpr (G::RAW_OBS) {
         if (c.valid) {
             uint8_t* o = obs + (row0 + c.lane) * G::OBS;
 #pragma unroll
@@ -144,17 +147,17 @@ __device__ __forceinline__ void emit_reward(float* reward, int64_t row, const fl
     }
 }
 
-template <int ROW, bool STAGED, int ROWS>
-struct ObsWords {
-    static constexpr int value = 1;
-};
-template <int ROW, int ROWS>
-struct ObsWords<ROW, true, ROWS> {
-    static constexpr int value = RowWriter<ROW, ROWS>::LDS_WORDS;
-};
+// LDS words of a wave's obs span image: bit rows (RowWriter, dword multiples), raw byte rows (RowWriterRaw, even)
+template <class G, int ROWS>
+constexpr int obs_lds_words()
+{
+    if constexpr (!G::RAW_OBS && G::OBS % 4 == 0) return RowWriter<G::OBS, ROWS>::LDS_WORDS;
+    else if constexpr (G::RAW_OBS && G::OBS % 2 == 0) return RowWriterRaw<G::OBS, ROWS>::LDS_WORDS;
+    else return 1;
+}
 template <class G, int ROWS = WAVE>
 struct ObsLds {
-    static constexpr int WORDS = ObsWords<G::OBS, !G::RAW_OBS && G::OBS % 4 == 0, ROWS>::value;
+    static constexpr int WORDS = obs_lds_words<G, ROWS>();
 };
 template <int W, int PAD, int ROWS, bool LDS>
 struct StageBytesOf {
@@ -420,7 +423,10 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
 }
 
 // ------------------------------------------------------------------------------------------------------------------
-static inline GameParams params_of(const Buffers& b) { return GameParams{b.num_players, b.num_decks}; }
+static inline GameParams params_of(const Buffers& b)
+{
+    return GameParams{b.num_players, b.num_decks, b.chips_for_each, b.dealer_id};
+}
 static inline dim3 grid_for(int64_t n, int epw = WAVE)
 {
     const int64_t per = (int64_t)WAVES_PER_BLOCK * epw;
@@ -484,6 +490,7 @@ int64_t stage_bytes_per_env(int32_t game, int32_t num_players)
     case CS_GAME_LEDUC: return stage_bytes_of<Leduc>();
     case CS_GAME_LIMIT: return stage_bytes_of<Limit>();
     case CS_GAME_BLACKJACK: return num_players <= 1 ? stage_bytes_of<Blackjack<1>>() : stage_bytes_of<Blackjack<4>>();
+    case CS_GAME_NOLIMIT: return stage_bytes_of<Nolimit>();
     default: return 0;
     }
 }
@@ -509,6 +516,13 @@ int game_info(int32_t game, const cs_config* cfg, cs_game_info* info)
         else fill_info<Blackjack<4>>(info);
         return CS_OK;
     }
+    case CS_GAME_NOLIMIT:
+        if (cfg && cfg->num_players != 0 && cfg->num_players != 2) return CS_E_UNSUPPORTED;
+        if (cfg && (cfg->chips_for_each < 0 || cfg->chips_for_each > 255 || cfg->dealer_plus1 < 0 ||
+                    cfg->dealer_plus1 > 2))
+            return CS_E_UNSUPPORTED;
+        fill_info<Nolimit>(info);
+        return CS_OK;
     case CS_GAME_DOUDIZHU:
         if (cfg && cfg->num_players != 0 && cfg->num_players != ddz::P) return CS_E_UNSUPPORTED;
         info->obs_dim = ddz::OBS;
@@ -528,6 +542,7 @@ int game_info(int32_t game, const cs_config* cfg, cs_game_info* info)
     switch (game) {                                              \
     case CS_GAME_LEDUC: return CALL(Leduc);                      \
     case CS_GAME_LIMIT: return CALL(Limit);                      \
+    case CS_GAME_NOLIMIT: return CALL(Nolimit);                  \
     case CS_GAME_BLACKJACK:                                      \
         switch (b.num_players) {                                 \
         case 1: return CALL(Blackjack<1>);                       \

@@ -116,6 +116,38 @@ __device__ inline uint32_t holdem_rank7(uint64_t cnt, uint64_t smp)
     return cat << 20 | v0 << 16 | v1 << 12 | v2 << 8 | v3 << 4 | v4;
 }
 
+// The hold'em deal (limitholdem/dealer.py: shuffle the 52-card deck, deal_card = pop()) of a heads-up game: hole i ->
+// player i % 2, card i / 2 from deck[51 - i]; flop deck[47..45], turn deck[44], river deck[43]. Fisher-Yates fixes
+// position i at step i, and only deck[43..51] is ever dealt, so the first nine swaps are tracked (swap k writes card vj
+// to position 51 - k -- dealt card D[k] -- and card vi to position j: JV[k] = j | vi << 8, looked up by the later
+// swaps) and the other 42 only consume their draws. Out: holes packed p0c0 | p0c1 << 6 | p1c0 << 12 | p1c1 << 18,
+// board c0..c4 6 bits each. Registers only (the rollout kernels' occupancy is register-bound).
+template <class Rng>
+__device__ __forceinline__ void holdem_deal2(Rng& rng, uint32_t& holes, uint32_t& board)
+{
+    uint32_t JV[9];
+    uint32_t d0 = 0, d1 = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        const uint32_t i = 51 - k;
+        const uint32_t j = rng.interval(i);
+        uint32_t vi = i, vj = j;
+#pragma unroll
+        for (int q = 0; q < k; q++) {   // oldest -> newest: the newest write to a position wins
+            const uint32_t jq = JV[q] & 255u, vq = JV[q] >> 8;
+            vi = jq == i ? vq : vi;
+            vj = jq == j ? vq : vj;
+        }
+        JV[k] = j | (vi << 8);
+        constexpr int F0[4] = {0, 12, 6, 18};   // hole i -> player i % 2, card i / 2
+        if (k < 4) d0 |= vj << F0[k < 4 ? k : 0];
+        else d1 |= vj << (6 * (k - 4));
+    }
+    rng.skip_intervals(42u);   // deck positions 42..1 are never dealt: only the words they consume matter
+    holes = d0;
+    board = d1;
+}
+
 struct Limit {
     static constexpr int OBS = 72, A = 4, P = 2, LB = 1, WORDS = 4, ACTION_BYTES = 1;
     static constexpr int NB = 3;
@@ -187,29 +219,8 @@ struct Limit {
     template <class Rng>
     __device__ __forceinline__ void reset(Rng& rng)
     {
-        // swap k writes card vj to position 51 - k (dealt: D[k]) and card vi to position j (JV[k] = j | vi << 8,
-        // looked up by the later swaps); D[k] goes straight into its packed field (registers: the rollout kernel's
-        // occupancy is register-bound here)
-        uint32_t JV[9];
-        uint32_t d0 = 0, d1 = 0;
-#pragma unroll
-        for (int k = 0; k < 9; k++) {
-            const uint32_t i = 51 - k;
-            const uint32_t j = rng.interval(i);
-            uint32_t vi = i, vj = j;
-#pragma unroll
-            for (int q = 0; q < k; q++) {   // oldest -> newest: the newest write to a position wins
-                const uint32_t jq = JV[q] & 255u, vq = JV[q] >> 8;
-                vi = jq == i ? vq : vi;
-                vj = jq == j ? vq : vj;
-            }
-            JV[k] = j | (vi << 8);
-            constexpr int F0[4] = {0, 12, 6, 18};   // hole i -> player i % 2, card i / 2 (w0 layout)
-            if (k < 4) d0 |= vj << F0[k < 4 ? k : 0];
-            else d1 |= vj << (6 * (k - 4));
-        }
-        rng.skip_intervals(42u);   // deck positions 42..1 are never dealt: only the words they consume matter
-        // hole i -> player i%2, card i/2, from deck[51-i] = D[i]
+        uint32_t d0, d1;
+        holdem_deal2(rng, d0, d1);
         const int s = (int)rng.interval(1u);
         const int in_0 = s == 0 ? 1 : 2, in_1 = s == 0 ? 2 : 1;
         const int first = s;  // (BB + 1) % 2 with BB = (s + 1) % 2

@@ -1,0 +1,202 @@
+// cs_nolimit.h -- No-limit Texas Hold'em (2 players) as a lane-per-env lockstep state machine.
+//
+// Behaviour (reference file:line):
+//   rlcard/games/nolimitholdem/game.py:45-56     configure: chips_for_each, dealer_id (None -> drawn by the first
+//                                                init_game and kept: the Game object outlives it)
+//   rlcard/games/nolimitholdem/game.py:58-110    init_game: dealer_id = randint(0, 2) if None, BEFORE the shuffle;
+//                                                deal as limit hold'em (holdem_deal2); SB = dealer + 1 bets 1, BB =
+//                                                dealer bets 2 (bets clamp to the stack); first actor BB + 1 = SB
+//   rlcard/games/nolimitholdem/round.py:62-130   proceed_round: CHECK_CALL / ALL_IN / RAISE_POT / RAISE_HALF_POT /
+//                                                FOLD; raised[] takes the unclamped amount; all-in status;
+//                                                not_raise_num / not_playing_num (never reset within a game)
+//   rlcard/games/nolimitholdem/round.py:132-165  legal actions (pot = sum of in_chips)
+//   rlcard/games/nolimitholdem/game.py:123-185   bypass rule, round end: pointer (dealer + 1) past bypassed players,
+//                                                flop / turn / river, skipped ahead while everyone is bypassed
+//   rlcard/games/limitholdem/game.py:216-231     is_over; nolimitholdem/game.py:226-236 payoffs in chips
+//   rlcard/games/limitholdem/judger.py:11-108    2 players: the winner nets min(in0, in1), a tie returns the bets
+//   rlcard/envs/nolimitholdem.py:54-85           obs[54] = card one-hot, my in_chips, max in_chips (raw bytes)
+// Illegal ids: the reference's fallback names a missing Action.CHECK and raises (envs/nolimitholdem.py:98-100); this
+// ABI plays CHECK_CALL (always legal) instead.
+// The stack is chips_for_each - in_chips (every bet moves chips from one to the other), so it is not stored.
+// Packed state, 4 u32 words per env (word-major [4][N]):
+//   w0: holes p0c0 p0c1 p1c0 p1c1 6 bits each (0..23), ptr (24), dealer (25), dealer drawn (26), rc:3 (27..29),
+//       over (31)
+//   w1: board c0..c4 6 bits each (0..29)
+//   w2: in0:8 in1:8 raised0:8 raised1:8
+//   w3: status0:2 status1:2 (0 alive, 1 folded, 2 all-in), not_raise_num:4 (4..7), not_playing_num:4 (8..11)
+#pragma once
+#include "cs_device.h"
+#include "cs_limit.h"
+
+#ifndef CS_NOLIMIT_MIN_WAVES
+#define CS_NOLIMIT_MIN_WAVES 5
+#endif
+
+namespace cs {
+
+struct Nolimit {
+    static constexpr int OBS = 54, A = 5, P = 2, LB = 1, WORDS = 4, ACTION_BYTES = 1;
+    static constexpr int NB = 14;               // raw obs bytes, four per word (RowWriterRaw)
+    static constexpr bool RAW_OBS = true;
+    static constexpr int SCRATCH_WORDS = 0;
+    // MT staging and launch shape as limit hold'em (same deal: ~72 draws per game)
+    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_PAD = 8, STAGE_R = 100;
+    static constexpr int RESTAGE_B = 8;
+    static constexpr int MIN_WAVES = CS_NOLIMIT_MIN_WAVES;
+    static constexpr int EPW = 32;
+    static constexpr int REFILL_K = 2;
+    enum { FOLD = 0, CHECK_CALL = 1, RAISE_HALF_POT = 2, RAISE_POT = 3, ALL_IN = 4 };
+    enum { ALIVE = 0, FOLDED = 1, ALLIN = 2 };
+
+    int chips, dealer_cfg;
+    uint32_t w0, w1, w2, w3;
+
+    __device__ __forceinline__ void bind(uint32_t*, const GameParams& prm)
+    {
+        chips = prm.chips_for_each;
+        dealer_cfg = prm.dealer_id;
+    }
+
+    __device__ __forceinline__ int hole(int p, int k) const { return (w0 >> (6 * (2 * p + k))) & 63; }
+    __device__ __forceinline__ int board(int k) const { return (w1 >> (6 * k)) & 63; }
+    __device__ __forceinline__ int ptr() const { return (w0 >> 24) & 1; }
+    __device__ __forceinline__ int rc() const { return (w0 >> 27) & 7; }
+    __device__ __forceinline__ int in(int p) const { return (w2 >> (8 * p)) & 255; }
+    __device__ __forceinline__ int raised(int p) const { return (w2 >> (16 + 8 * p)) & 255; }
+    __device__ __forceinline__ int status(int p) const { return (w3 >> (2 * p)) & 3; }
+
+    __device__ __forceinline__ void load(const uint32_t* st, int64_t n, int64_t env)
+    {
+        w0 = st[env]; w1 = st[n + env]; w2 = st[2 * n + env]; w3 = st[3 * n + env];
+    }
+    __device__ __forceinline__ void store(uint32_t* st, int64_t n, int64_t env) const
+    {
+        st[env] = w0; st[n + env] = w1; st[2 * n + env] = w2; st[3 * n + env] = w3;
+    }
+    __device__ __forceinline__ void blank() { w0 = 1u << 31; w1 = 0; w2 = 0; w3 = 0; }
+
+    __device__ __forceinline__ int current() const { return ptr(); }
+    __device__ __forceinline__ bool is_over() const { return (w0 >> 31) != 0; }
+
+    // round.py:132-165 for the player at the pointer
+    __device__ __forceinline__ uint32_t legal() const
+    {
+        const int p = ptr(), r0 = raised(0), r1 = raised(1), mx = r0 > r1 ? r0 : r1, rp = p ? r1 : r0;
+        const int rem = chips - in(p), pot = in(0) + in(1), half = pot >> 1, diff = mx - rp;
+        uint32_t m = 0x1F;
+        if (diff > 0 && diff >= rem) {
+            m = (1u << FOLD) | (1u << CHECK_CALL);
+        } else {
+            if (pot > rem) m &= ~(1u << RAISE_POT);
+            if (half > rem || half + rp <= mx) m &= ~(1u << RAISE_HALF_POT);
+        }
+        return m;
+    }
+
+    __device__ __forceinline__ void observe(int player, uint32_t (&raw)[NB]) const
+    {
+        uint64_t cards = 0;
+        const int r = rc(), npub = r == 0 ? 0 : (r + 2 < 5 ? r + 2 : 5);
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+            if (k < npub) cards |= 1ull << board(k);
+        cards |= 1ull << hole(player, 0);
+        cards |= 1ull << hole(player, 1);
+#pragma unroll
+        for (int j = 0; j < 13; j++) raw[j] = RowWriter<4>::expand4((uint32_t)(cards >> (4 * j)) & 15u);
+        const int a = in(0), b = in(1);
+        raw[13] = (uint32_t)(player ? b : a) | (uint32_t)(a > b ? a : b) << 8;
+    }
+
+    template <class Rng>
+    __device__ __forceinline__ void reset(Rng& rng)
+    {
+        int dealer;
+        if (dealer_cfg >= 0) dealer = dealer_cfg;
+        else if ((w0 >> 26) & 1) dealer = (w0 >> 25) & 1;     // drawn by an earlier game of this env
+        else dealer = (int)rng.interval(1u);                  // randint(0, 2), before the deal
+        uint32_t holes, brd;
+        holdem_deal2(rng, holes, brd);
+        const int s = dealer ^ 1, b = dealer;            // SB (dealer + 1), BB (dealer + 2) = dealer
+        const int bb = chips < 2 ? chips : 2, sb = chips < 1 ? chips : 1;
+        const int i0 = b == 0 ? bb : sb, i1 = b == 0 ? sb : bb;
+        w0 = holes | (uint32_t)s << 24 | (uint32_t)dealer << 25 | 1u << 26;   // first actor BB + 1 = SB; rc 0
+        w1 = brd;
+        w2 = (uint32_t)i0 | (uint32_t)i1 << 8 | (uint32_t)i0 << 16 | (uint32_t)i1 << 24;   // raised = in_chips
+        w3 = 0;
+    }
+
+    template <class Rng>
+    __device__ __forceinline__ void step(int a, Rng&)
+    {
+        const uint32_t lg = legal();
+        if (a < 0 || a > 4 || !((lg >> a) & 1u)) a = CHECK_CALL;
+        int p = ptr(), r = rc();
+        int i0 = in(0), i1 = in(1), ra0 = raised(0), ra1 = raised(1), s0 = status(0), s1 = status(1);
+        int nrn = (w3 >> 4) & 15, npn = (w3 >> 8) & 15;
+        const int mx = ra0 > ra1 ? ra0 : ra1, pot = i0 + i1;
+        int ip = p ? i1 : i0, rp = p ? ra1 : ra0, sp = p ? s1 : s0;
+        int want = 0;                                    // chips asked for; bet() clamps to the stack
+        if (a == CHECK_CALL) { want = mx - rp; rp = mx; nrn += 1; }
+        else if (a == ALL_IN) { want = chips - ip; rp += want; nrn = 1; }
+        else if (a == RAISE_POT) { want = pot; rp += pot; nrn = 1; }
+        else if (a == RAISE_HALF_POT) { want = pot >> 1; rp += want; nrn = 1; }
+        else { sp = FOLDED; }
+        const int rem = chips - ip;
+        ip += want < rem ? want : rem;
+        if (ip == chips && sp != FOLDED) sp = ALLIN;
+        if (sp == ALLIN) { npn += 1; nrn -= 1; }
+        if (sp == FOLDED) npn += 1;
+        if (p) { i1 = ip; ra1 = rp; s1 = sp; } else { i0 = ip; ra0 = rp; s0 = sp; }
+        p ^= 1;
+        if ((p ? s1 : s0) == FOLDED) p ^= 1;
+        // game.py:135-141 bypass: folded / all-in players, and the last other one if already level
+        int by0 = s0 != ALIVE, by1 = s1 != ALIVE;
+        if (by0 + by1 == 1) {
+            const int m2 = ra0 > ra1 ? ra0 : ra1;
+            if (!by0 && ra0 >= m2) by0 = 1;
+            else if (!by1 && ra1 >= m2) by1 = 1;
+        }
+        if (nrn + npn >= 2) {                            // round over: deal and start the next betting round
+            const int all = by0 && by1;
+            p = (((w0 >> 25) & 1) + 1) & 1;              // dealer + 1, past bypassed players unless all are
+            if (!all && (p ? by1 : by0)) p ^= 1;
+            if (all) r = 4;                              // flop, turn and river all dealt (rc 0/1/2 -> 4)
+            else r += 1;                                 // rc 0 -> flop, 1 -> turn, 2 -> river, 3 -> none
+            ra0 = 0; ra1 = 0; nrn = 0;
+        }
+        const int over = (s0 == FOLDED) + (s1 == FOLDED) == 1 || r >= 4;
+        w0 = (w0 & 0x06FFFFFFu) | (uint32_t)p << 24 | (uint32_t)r << 27 | (uint32_t)over << 31;
+        w2 = (uint32_t)i0 | (uint32_t)i1 << 8 | (uint32_t)ra0 << 16 | (uint32_t)ra1 << 24;
+        w3 = (uint32_t)s0 | (uint32_t)s1 << 2 | (uint32_t)(nrn & 15) << 4 | (uint32_t)(npn & 15) << 8;
+    }
+
+    __device__ __forceinline__ void payoffs(float (&out)[P]) const
+    {
+        const int s0 = status(0), s1 = status(1);
+        int win0, win1;
+        if (s0 == FOLDED || s1 == FOLDED) {
+            win0 = s0 != FOLDED; win1 = s1 != FOLDED;
+        } else {
+            uint64_t bc = 0, bs = 0;
+#pragma unroll
+            for (int k = 0; k < 5; k++) tally_card(board(k), bc, bs);
+            uint64_t c0 = bc, q0 = bs;
+            tally_card(hole(0, 0), c0, q0);
+            tally_card(hole(0, 1), c0, q0);
+            const uint32_t v0 = holdem_rank7(c0, q0);
+            uint64_t c1 = bc, q1 = bs;
+            tally_card(hole(1, 0), c1, q1);
+            tally_card(hole(1, 1), c1, q1);
+            const uint32_t v1 = holdem_rank7(c1, q1);
+            win0 = v0 >= v1; win1 = v1 >= v0;
+        }
+        const int a = in(0), b = in(1), m = a < b ? a : b;
+        float p0 = 0.f;
+        if (!(win0 && win1)) p0 = win0 ? (float)m : -(float)m;
+        out[0] = p0;
+        out[1] = -p0;
+    }
+};
+
+}  // namespace cs

@@ -1,4 +1,4 @@
-"""rlcard's env registry (rlcard/envs/registration.py:8-89 + envs/__init__.py) for the engine's four games."""
+"""rlcard's env registry (rlcard/envs/registration.py:8-89 + envs/__init__.py) for the engine's five games."""
 import importlib
 
 DEFAULT_CONFIG = {'allow_step_back': False, 'seed': None}
@@ -49,3 +49,4 @@ register('blackjack', 'rlcard_amd.envs.blackjack:BlackjackEnv')
 register('leduc-holdem', 'rlcard_amd.envs.leducholdem:LeducholdemEnv')
 register('limit-holdem', 'rlcard_amd.envs.limitholdem:LimitholdemEnv')
 register('doudizhu', 'rlcard_amd.envs.doudizhu:DoudizhuEnv')
+register('no-limit-holdem', 'rlcard_amd.envs.nolimitholdem:NolimitholdemEnv')

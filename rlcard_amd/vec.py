@@ -57,7 +57,8 @@ class VecEnv:
             raise _abi.CardsimError('VecEnv runs on the GPU only (got device %s)' % self.device)
         np_ = int(config.get('game_num_players', 0))
         nd = int(config.get('game_num_decks', -1))
-        self.info, self.cfg = _abi.game_info(self.game, np_, nd)
+        chips = int(config.get('chips_for_each', 0))
+        self.info, self.cfg = _abi.game_info(self.game, np_, nd, chips, config.get('dealer_id'))
         self.obs_dim = self.info.obs_dim
         self.num_actions = self.info.num_actions
         self.num_players = self.info.num_players

@@ -15,6 +15,8 @@ Fixtures written:
                    to pin _decode_action's fallback), obs, legal-action bitmask, next player, done, payoffs,
                    and the final obs of every player (Env.run appends them, rlcard/envs/env.py:161-164).
   limit.npz        same for limit-holdem (pins the stale raise_nums quirk of limitholdem/game.py:98/:101).
+  nolimit.npz      same for no-limit-holdem under four configs (chips_for_each / dealer_id per env: env_chips,
+                   env_dealer; -1 = dealer drawn by the game).
   blackjack.npz    same for blackjack (+ the config-1 run_random.py trajectory: env seed 42, np.random.seed(42)).
   doudizhu.npz     same for doudizhu (legal ids as CSR, obs padded to 901).
   holdem_eval.npz  compare_hands winner KATs on random and category-dense 7-card deals (limitholdem/utils.py).
@@ -176,12 +178,12 @@ class Stream:
 
 def drive(env_id, config, seeds, games, stream, pick, extra_keys=()):
     """For each seed: make the env once (its RNG stream continues across resets, as in the reference), then play
-    `games` games, choosing each action with pick(rng, state, env)."""
+    `games` games, choosing each action with pick(rng, state, env). config: one dict, or one per seed."""
     import random
     import rlcard
     game_counter = 0
     for ei, seed in enumerate(seeds):
-        cfg = dict(config)
+        cfg = dict(config[ei] if isinstance(config, (list, tuple)) else config)
         cfg['seed'] = int(seed)
         env = rlcard.make(env_id, config=cfg)
         rng = random.Random(1000003 * (ei + 1) + int(seed))
@@ -263,6 +265,25 @@ def gen_doudizhu():
     drive('doudizhu', {}, seeds, 4, st, pick)
     st.save(os.path.join(OUT, 'doudizhu.npz'), seeds)
     print('doudizhu.npz: %d events' % len(st.obs))
+
+
+def gen_nolimit():
+    """No-limit hold'em (rlcard/games/nolimitholdem/, envs/nolimitholdem.py): the default config plus short stacks
+    (more all-ins: the bypass deal of game.py:137-171, side-pot judging) and a fixed dealer. Only legal ids are fed:
+    the reference's _decode_action fallback names Action.CHECK, which does not exist (envs/nolimitholdem.py:98-100),
+    so an illegal id raises there."""
+    seeds = [0, 1, 7, 42, 12941, 3, 42, 5, 9]
+    cfgs = [{}] * 5 + [{'chips_for_each': 12, 'dealer_id': 1}] * 2 + [{'chips_for_each': 3}, {'chips_for_each': 40,
+                                                                                            'dealer_id': 0}]
+    st = Stream(54, 5, 2)
+
+    def pick(rng, state, env):
+        return rng.choice(sorted(state['legal_actions'].keys()))
+    drive('no-limit-holdem', cfgs, seeds, 60, st, pick)
+    st.save(os.path.join(OUT, 'nolimit.npz'), seeds,
+            env_chips=np.array([c.get('chips_for_each', 100) for c in cfgs], dtype=np.int32),
+            env_dealer=np.array([c.get('dealer_id', -1) for c in cfgs], dtype=np.int32))
+    print('nolimit.npz: %d events' % len(st.obs))
 
 
 # --------------------------------------------------------------------------------------------------------------
@@ -420,7 +441,7 @@ def main():
     args = ap.parse_args()
     setup_reference()
     gens = {'mt19937': gen_mt, 'leduc': gen_leduc, 'limit': gen_limit, 'blackjack': gen_blackjack,
-            'doudizhu': gen_doudizhu, 'holdem_eval': gen_holdem_eval, 'ddz_table': gen_ddz_table,
+            'doudizhu': gen_doudizhu, 'nolimit': gen_nolimit, 'holdem_eval': gen_holdem_eval, 'ddz_table': gen_ddz_table,
             'ddz_judger': gen_ddz_judger}
     for name, fn in gens.items():
         if args.only is None or name in args.only:

@@ -11,6 +11,23 @@ def load(name):
     return np.load(os.path.join(GOLDEN, name + '.npz'), allow_pickle=False)
 
 
+def env_config(d, ei):
+    """Game config of fixture env ei (nolimit.npz holds one per env; the other streams use the defaults)."""
+    if 'env_chips' not in d.files:
+        return {}
+    dealer = int(d['env_dealer'][ei])
+    return {'chips_for_each': int(d['env_chips'][ei]), 'dealer_id': None if dealer < 0 else dealer}
+
+
+def config_groups(d):
+    """[(config, [env index, ...])]: fixture envs grouped by game config (a VecEnv has one config)."""
+    groups = {}
+    for ei in range(len(d['seeds'])):
+        c = env_config(d, ei)
+        groups.setdefault(tuple(sorted(c.items())), (c, []))[1].append(ei)
+    return list(groups.values())
+
+
 def legal_bits_of(d, k, num_actions):
     if 'ev_legal' in d.files:
         return d['ev_legal'][k]

@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(ROOT, 'oracle', 'liboracle.so')
 GOLDEN = os.path.join(ROOT, 'tests', 'golden')
 
-GAMES = {'blackjack': 0, 'leduc-holdem': 1, 'limit-holdem': 2, 'doudizhu': 3}
+GAMES = {'blackjack': 0, 'leduc-holdem': 1, 'limit-holdem': 2, 'doudizhu': 3, 'no-limit-holdem': 4}
 
 _lib = None
 
@@ -26,7 +26,8 @@ class MT(C.Structure):
 
 
 class Cfg(C.Structure):
-    _fields_ = [('num_players', C.c_int32), ('num_decks', C.c_int32)]
+    _fields_ = [('num_players', C.c_int32), ('num_decks', C.c_int32), ('chips_for_each', C.c_int32),
+                ('dealer_id', C.c_int32)]
 
 
 class Info(C.Structure):
@@ -85,11 +86,11 @@ def load_ddz_table():
 class Batch:
     """Oracle batch with the C-ABI semantics; outputs as numpy arrays."""
 
-    def __init__(self, game, n, keys, key_len, num_players=None, num_decks=1):
+    def __init__(self, game, n, keys, key_len, num_players=None, num_decks=1, chips_for_each=100, dealer_id=-1):
         L = lib()
         self.game = GAMES[game] if isinstance(game, str) else game
-        np_ = num_players if num_players is not None else {0: 1, 1: 2, 2: 2, 3: 3}[self.game]
-        self.cfg = Cfg(np_, num_decks)
+        np_ = num_players if num_players is not None else {0: 1, 1: 2, 2: 2, 3: 3, 4: 2}[self.game]
+        self.cfg = Cfg(np_, num_decks, chips_for_each, dealer_id)
         self.info = Info()
         if L.or_game_info(self.game, C.byref(self.cfg), C.byref(self.info)) != 0:
             raise ValueError('bad game config')

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_game_info_shapes():
     shapes = {'leduc-holdem': (36, 4, 2, 1, 1), 'limit-holdem': (72, 4, 2, 1, 1), 'blackjack': (2, 2, 1, 1, 1),
-              'doudizhu': (901, 27472, 3, 3434, 2)}
+              'doudizhu': (901, 27472, 3, 3434, 2), 'no-limit-holdem': (54, 5, 2, 1, 1)}
     for game, (o, a, p, lb, ab) in shapes.items():
         info, _ = _abi.game_info(game)
         assert (info.obs_dim, info.num_actions, info.num_players, info.legal_bytes, info.action_bytes) == \

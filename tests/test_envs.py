@@ -11,8 +11,10 @@ import rlcard_amd
 from rlcard_amd.envs import doudizhu as ddz_env
 
 torch = pytest.importorskip('torch')
-GAMES = [('leduc-holdem', 'leduc'), ('limit-holdem', 'limit'), ('blackjack', 'blackjack'), ('doudizhu', 'doudizhu')]
+GAMES = [('leduc-holdem', 'leduc'), ('limit-holdem', 'limit'), ('blackjack', 'blackjack'), ('doudizhu', 'doudizhu'),
+         ('no-limit-holdem', 'nolimit')]
 SHAPES = {'leduc-holdem': (2, 4, [[36]] * 2, np.float64), 'limit-holdem': (2, 4, [[72]] * 2, np.float64),
+          'no-limit-holdem': (2, 5, [[54]] * 2, np.float64),
           'blackjack': (1, 2, [[2]], np.int64), 'doudizhu': (3, 27472, [[790], [901], [901]], np.int8)}
 
 
@@ -60,8 +62,8 @@ def test_blackjack_run_random_config1_matches_reference_trajectory():
 
 class _Adapter:
     """One compat Env in the shape golden_replay.replay expects."""
-    def __init__(self, game, seed):
-        self.env = rlcard_amd.make(game, config={'seed': seed})
+    def __init__(self, game, seed, config=None):
+        self.env = rlcard_amd.make(game, config=dict(config or {}, seed=seed))
 
     def _pack(self, state, player, done):
         bits = np.zeros(self.env.num_actions, np.uint8)
@@ -87,7 +89,7 @@ class _Adapter:
 @pytest.mark.parametrize('game,name', GAMES)
 def test_reference_stream_through_compat_env(game, name):
     d = gr.load(name)
-    assert gr.replay(d, lambda ei, s: _Adapter(game, s), SHAPES[game][1]) == len(d['ev_kind'])
+    assert gr.replay(d, lambda ei, s: _Adapter(game, s, gr.env_config(d, ei)), SHAPES[game][1]) == len(d['ev_kind'])
 
 
 @pytest.mark.gpu

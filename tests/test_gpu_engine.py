@@ -8,13 +8,13 @@ from rlcard_amd import seeding
 torch = pytest.importorskip('torch')
 pytestmark = pytest.mark.gpu
 
-GAMES = [('leduc-holdem', 'leduc'), ('limit-holdem', 'limit'), ('blackjack', 'blackjack'), ('doudizhu', 'doudizhu')]
-LANE_GAMES = GAMES[:3]
+GAMES = [('leduc-holdem', 'leduc'), ('limit-holdem', 'limit'), ('blackjack', 'blackjack'), ('doudizhu', 'doudizhu'),
+         ('no-limit-holdem', 'nolimit')]
 # doudizhu runs one wave per env and its oracle scans the 27 472-id table per observation: smaller parity batches
 STEP_SIZE = {'doudizhu': (130, 40)}            # (envs, steps); default (3000, 120)
 ROLL_SIZE = {'doudizhu': (130, 24)}            # (envs, T); default (4197, 48)
 FULL_SIZE = {'leduc-holdem': (1 << 20, 16, 384), 'limit-holdem': (262144, 16, 384), 'blackjack': (262144, 16, 384),
-             'doudizhu': (65536, 8, 64)}      # (envs, T, oracle window)
+             'doudizhu': (65536, 8, 64), 'no-limit-holdem': (262144, 16, 384)}      # (envs, T, oracle window)
 
 
 def _np(o):
@@ -37,8 +37,8 @@ def test_single_env_replays_reference_stream(game, name):
     d = gr.load(name)
 
     class One:
-        def __init__(self, seed):
-            self.v = _vec(game, 1, seeds=[seed])
+        def __init__(self, ei, seed):
+            self.v = _vec(game, 1, seeds=[seed], config=gr.env_config(d, ei))
 
         def reset(self):
             return {k: x[0] for k, x in _np(self.v.reset()).items()}
@@ -51,16 +51,21 @@ def test_single_env_replays_reference_stream(game, name):
             return o['obs'][0], o['legal'][0]
 
     num_actions = _vec(game, 1).num_actions
-    assert gr.replay(d, lambda ei, s: One(s), num_actions) == len(d['ev_kind'])
+    assert gr.replay(d, One, num_actions) == len(d['ev_kind'])
 
 
 @pytest.mark.parametrize('game,name', GAMES)
 def test_batched_replay_with_lazy_reset(game, name):
     """All fixture seeds as one batch; a 'reset' event after a finished game is a step with any action (lazy reset)."""
     d = gr.load(name)
-    seeds = [int(s) for s in d['seeds']]
-    v = _vec(game, len(seeds), seeds=seeds)
-    per_env = [np.nonzero(d['ev_env'] == i)[0] for i in range(len(seeds))]
+    for cfg, envs in gr.config_groups(d):
+        _batched_replay(d, cfg, envs, game)
+
+
+def _batched_replay(d, cfg, envs, game):
+    seeds = [int(d['seeds'][i]) for i in envs]
+    v = _vec(game, len(seeds), seeds=seeds, config=cfg)
+    per_env = [np.nonzero(d['ev_env'] == i)[0] for i in envs]
     ticks = max(len(x) for x in per_env)
     out = _np(v.reset())
     for tick in range(ticks):
@@ -179,6 +184,12 @@ def test_full_size_rollout_properties_and_sampled_parity(oracle, game, name):
     if game == 'limit-holdem':
         s = tr['obs'].long().sum(-1)
         assert bool(((s >= 6) & (s <= 11)).all()), 'limit obs: 2 hole + 0/3/4/5 board + 4 raise slots'
+    if game == 'no-limit-holdem':
+        s = tr['obs'][..., :52].long().sum(-1)
+        assert bool(((s == 2) | (s == 5) | (s == 6) | (s == 7)).all()), 'no-limit obs: 2 hole + 0/3/4/5 board'
+        mine, top = tr['obs'][..., 52].long(), tr['obs'][..., 53].long()
+        assert bool(((mine >= 1) & (mine <= top) & (top <= 100)).all()), 'chips: 1 <= mine <= max <= stack'
+        assert bool((tr['reward'][done].abs() <= 100).all())
     # exact parity on three windows (start, middle, end) replayed by the oracle with the same env ids
     for start in (0, n // 2 + 17, n - win):
         ob = _oracle_batch(oracle, game, range(42 + start, 42 + start + win))

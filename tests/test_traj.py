@@ -8,7 +8,7 @@ from rlcard_amd import seeding
 torch = pytest.importorskip('torch')
 pytestmark = pytest.mark.gpu
 
-GAMES = ['leduc-holdem', 'limit-holdem', 'blackjack', 'doudizhu']
+GAMES = ['leduc-holdem', 'limit-holdem', 'blackjack', 'doudizhu', 'no-limit-holdem']
 SIZE = {'doudizhu': (70, 40)}   # (envs, T); default (700, 48)
 
 
