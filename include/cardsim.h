@@ -148,6 +148,19 @@ int cs_legal_lists(cs_handle* h, const void* legal, int64_t rows, int32_t* count
  * envs/doudizhu.py:136-142; other games one-hot of num_actions, envs/env.py:211-220): u8 [count][action_feature_dim]. */
 int cs_action_features(cs_handle* h, const int32_t* ids, int64_t count, void* features, void* stream);
 
+/* Chance-sampling CFR on Leduc Hold'em (rlcard/agents/cfr_agent.py:30-123) over this handle's envs: `iterations` x
+ * CFRAgent.train(). Per iteration, for each player, every env deals a new game from its own stream (Env.reset) and
+ * the whole betting tree under that deal is traversed with the reference's step / step_back recursion (traverse_tree),
+ * accumulating regrets and the average policy; then regret matching updates the policy (update_policy). Tables are
+ * caller-owned DEVICE buffers indexed by the Leduc observation the reference keys its dicts with
+ * (((hand * 4 + public + 1) * 15 + my chips) * 15 + others' chips, 2700 rows): policy / average_policy / regrets
+ * double [2700][4] (policy initialised to 0.25 = the reference's row for an unseen key), flags uint32 [2700] (bit 0:
+ * key in policy, bit 1: key in regrets and average_policy), zero-initialised. iteration0 = the agent's iteration
+ * count before this call. A 1-env handle is the reference agent, bit-exact (same fp64 operation order); with more
+ * envs, each deals its own game per player per iteration and the tables accumulate in fp64 atomics. Leduc only. */
+int cs_cfr_train(cs_handle* h, int32_t iterations, int64_t iteration0, double* policy, double* average_policy,
+                 double* regrets, uint32_t* flags, void* stream);
+
 /* Copy the packed state words of env `env` (state_words u32, HOST buffer) -- the raw fields behind
  * Env.get_state()['raw_obs'] / get_perfect_information for single-env compatibility and debugging. Synchronous. */
 int cs_get_env_state(cs_handle* h, int64_t env, uint32_t* host_words, int32_t nwords);

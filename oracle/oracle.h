@@ -83,6 +83,16 @@ void or_batch_rollout(or_batch *b, int32_t T, uint64_t policy_seed, uint64_t t0,
 /* total u32 draws consumed so far by env i (for RNG-position parity checks) */
 uint64_t or_batch_draws(or_batch *b, int64_t env);
 
+/* ---- chance-sampling CFR on Leduc Hold'em (agents/cfr_agent.py), or_cfr.c ----------------------------------- */
+#define OR_CFR_INFOSETS 2700   /* dense infoset table: ((hand * 4 + public + 1) * 15 + my chips) * 15 + others' */
+typedef struct or_cfr or_cfr;
+int or_cfr_infoset(const uint8_t *obs /* Leduc obs[36] */);
+or_cfr *or_cfr_create(int64_t n, const uint32_t *keys /* [n][2] */, const int32_t *key_len);
+void or_cfr_destroy(or_cfr *c);
+void or_cfr_train(or_cfr *c, int32_t iterations);           /* `iterations` x CFRAgent.train()              */
+void or_cfr_tables(const or_cfr *c, double *policy, double *avg, double *regrets, uint8_t *flags); /* [2700][4] */
+uint64_t or_cfr_draws(const or_cfr *c, int64_t env);
+
 /* ---- hold'em evaluator (limitholdem/utils.py compare_hands) ---------------------------------------------------- */
 /* cards: 7 card indices (card2index order: suit-major S,H,D,C; rank A..K). Returns a value whose order is
  * the reference's hand order (equal values = split). */

@@ -1,1 +1,2 @@
 from .random_agent import RandomAgent  # noqa: F401
+from .cfr_agent import CFRAgent  # noqa: F401

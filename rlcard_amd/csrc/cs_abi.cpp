@@ -190,6 +190,20 @@ int cs_observe(cs_handle* h, int32_t player, const cs_step_out* out, void* strea
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_observe");
 }
 
+int cs_cfr_train(cs_handle* h, int32_t iterations, int64_t iteration0, double* policy, double* average_policy,
+                 double* regrets, uint32_t* flags, void* stream)
+{
+    if (!h || !policy || !average_policy || !regrets || !flags) return fail(CS_E_INVALID, "null argument");
+    if (h->b.game != CS_GAME_LEDUC) return fail(CS_E_UNSUPPORTED, "cs_cfr_train supports leduc-holdem only");
+    if (iterations < 0 || iteration0 < 0) return fail(CS_E_INVALID, "negative iteration count");
+    if (!h->seeded) return fail(CS_E_STATE, "cs_cfr_train before cs_seed");
+    int r = set_device(h);
+    if (r != CS_OK) return r;
+    const cs::CfrTables t{policy, average_policy, regrets, flags};
+    hipError_t e = cs::launch_cfr(h->b, iterations, iteration0, t, (hipStream_t)stream);
+    return e == hipSuccess ? CS_OK : fail_hip(e, "cs_cfr_train");
+}
+
 int cs_rollout(cs_handle* h, int32_t T, uint64_t policy_seed, uint64_t t0, uint64_t env_base, const cs_traj_out* out,
                void* stream)
 {

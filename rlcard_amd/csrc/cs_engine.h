@@ -34,6 +34,16 @@ hipError_t launch_observe(const Buffers& b, int32_t player, const cs_step_out& o
 hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
                           const cs_traj_out& o, hipStream_t s);
 
+// cs_cfr.hip: chance-sampling CFR tables on Leduc (device pointers, [CFR_NI][4] fp64 + [CFR_NI] u32 flags)
+constexpr int CFR_NI = 2700;
+struct CfrTables {
+    double* policy;
+    double* avg;
+    double* regrets;
+    uint32_t* flags;
+};
+hipError_t launch_cfr(const Buffers& b, int32_t iterations, int64_t iteration0, const CfrTables& t, hipStream_t s);
+
 // cs_traj.hip
 hipError_t launch_transitions(const Buffers& b, int32_t T, const cs_traj_out& tr, const cs_trans_out& o,
                               hipStream_t s);

@@ -134,6 +134,15 @@ class Env(object):
         self._last = None
         return s
 
+    def _sync_from_engine(self):
+        """Re-read the env's current game from the engine after device-side work that moved it (cs_cfr_train leaves
+        the last deal at its root, as the reference's traversal leaves its env after stepping every step back)."""
+        o = self._host(self._vec.observe(0))
+        if o['player'] != 0:
+            o = self._host(self._vec.observe(o['player']))
+        o['reward'] = np.zeros(self.num_players, np.float32)
+        self._last, self._payoffs, self._history = o, None, []
+
     # -- engine row -> reference types ---------------------------------------------------------------------------
     @staticmethod
     def _host(o):

@@ -19,6 +19,7 @@ Fixtures written:
                    env_dealer; -1 = dealer drawn by the game).
   blackjack.npz    same for blackjack (+ the config-1 run_random.py trajectory: env seed 42, np.random.seed(42)).
   doudizhu.npz     same for doudizhu (legal ids as CSR, obs padded to 901).
+  cfr.npz          CFRAgent tables (policy, average_policy, regrets; keys = obs) after K train() iterations.
   holdem_eval.npz  compare_hands winner KATs on random and category-dense 7-card deals (limitholdem/utils.py).
   ddz_judger.npz   (hand, previous play) -> legal id sets from Judger / get_gt_cards (doudizhu/judger.py, utils.py).
 
@@ -286,6 +287,31 @@ def gen_nolimit():
     print('nolimit.npz: %d events' % len(st.obs))
 
 
+def gen_cfr():
+    """The reference CFRAgent (agents/cfr_agent.py, chance sampling) trained on leduc-holdem envs with
+    allow_step_back: its policy / average_policy / regrets dicts (keys = float64 obs bytes, 36 one-hot values) after
+    K iterations, as arrays. Deals come from the env's own RandomState (one Env.reset per player per iteration)."""
+    import rlcard
+    from rlcard.agents.cfr_agent import CFRAgent
+    runs = [(0, 25), (5, 12), (42, 40)]
+    out = {}
+    for r, (seed, iters) in enumerate(runs):
+        env = rlcard.make('leduc-holdem', config={'seed': seed, 'allow_step_back': True})
+        agent = CFRAgent(env, model_path=os.path.join(WORK, 'cfr_model'))
+        for _ in range(iters):
+            agent.train()
+        for name in ('policy', 'average_policy', 'regrets'):
+            d = getattr(agent, name)
+            keys = sorted(d.keys())
+            obs = np.stack([np.frombuffer(k, dtype=np.float64) for k in keys]).astype(np.uint8)
+            assert obs.shape[1] == 36
+            out['r%d_%s_obs' % (r, name)] = obs
+            out['r%d_%s_val' % (r, name)] = np.stack([np.asarray(d[k], dtype=np.float64) for k in keys])
+    np.savez_compressed(os.path.join(OUT, 'cfr.npz'), seeds=np.array([s for s, _ in runs], np.int64),
+                        iterations=np.array([k for _, k in runs], np.int64), **out)
+    print('cfr.npz: %s' % ', '.join('seed %d x %d it' % x for x in runs))
+
+
 # --------------------------------------------------------------------------------------------------------------
 # Hold'em evaluator KATs (compare_hands, rlcard/games/limitholdem/utils.py:526-614)
 # --------------------------------------------------------------------------------------------------------------
@@ -441,7 +467,7 @@ def main():
     args = ap.parse_args()
     setup_reference()
     gens = {'mt19937': gen_mt, 'leduc': gen_leduc, 'limit': gen_limit, 'blackjack': gen_blackjack,
-            'doudizhu': gen_doudizhu, 'nolimit': gen_nolimit, 'holdem_eval': gen_holdem_eval, 'ddz_table': gen_ddz_table,
+            'doudizhu': gen_doudizhu, 'nolimit': gen_nolimit, 'cfr': gen_cfr, 'holdem_eval': gen_holdem_eval, 'ddz_table': gen_ddz_table,
             'ddz_judger': gen_ddz_judger}
     for name, fn in gens.items():
         if args.only is None or name in args.only:

@@ -65,6 +65,14 @@ def lib():
         L.or_batch_rollout.argtypes = [C.c_void_p, C.c_int32, C.c_uint64, C.c_uint64, C.c_uint64] + [C.c_void_p] * 7
         L.or_batch_draws.argtypes = [C.c_void_p, C.c_int64]
         L.or_batch_draws.restype = C.c_uint64
+        L.or_cfr_infoset.argtypes = [C.c_void_p]
+        L.or_cfr_create.argtypes = [C.c_int64, C.c_void_p, C.c_void_p]
+        L.or_cfr_create.restype = C.c_void_p
+        L.or_cfr_destroy.argtypes = [C.c_void_p]
+        L.or_cfr_train.argtypes = [C.c_void_p, C.c_int32]
+        L.or_cfr_tables.argtypes = [C.c_void_p] * 5
+        L.or_cfr_draws.argtypes = [C.c_void_p, C.c_int64]
+        L.or_cfr_draws.restype = C.c_uint64
         L.or_holdem_rank7.argtypes = [C.c_void_p]
         L.or_holdem_rank7.restype = C.c_uint32
         L.or_ddz_set_table.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
@@ -143,3 +151,38 @@ class Batch:
 
     def draws(self, env):
         return lib().or_batch_draws(self.h, env)
+
+
+CFR_INFOSETS = 2700
+
+
+class CFR:
+    """Oracle chance-sampling CFR (oracle/or_cfr.c) over n Leduc envs; n = 1 is the reference CFRAgent."""
+
+    def __init__(self, keys, key_len):
+        keys = np.ascontiguousarray(keys, dtype=np.uint32).reshape(-1, 2)
+        key_len = np.ascontiguousarray(key_len, dtype=np.int32).reshape(-1)
+        self.n = len(key_len)
+        self.h = lib().or_cfr_create(self.n, P(keys), P(key_len))
+
+    def __del__(self):
+        if getattr(self, 'h', None):
+            lib().or_cfr_destroy(self.h)
+            self.h = None
+
+    def train(self, iterations=1):
+        lib().or_cfr_train(self.h, int(iterations))
+
+    def tables(self):
+        t = dict(policy=np.zeros((CFR_INFOSETS, 4)), average_policy=np.zeros((CFR_INFOSETS, 4)),
+                 regrets=np.zeros((CFR_INFOSETS, 4)), flags=np.zeros(CFR_INFOSETS, np.uint8))
+        lib().or_cfr_tables(self.h, P(t['policy']), P(t['average_policy']), P(t['regrets']), P(t['flags']))
+        return t
+
+    def draws(self, env):
+        return lib().or_cfr_draws(self.h, env)
+
+
+def cfr_infoset(obs):
+    o = np.ascontiguousarray(obs, dtype=np.uint8)
+    return lib().or_cfr_infoset(P(o))

@@ -1,0 +1,114 @@
+"""Chance-sampling CFR on Leduc (rlcard/agents/cfr_agent.py) on the GPU: the reference agent's
+tables after K iterations (tests/golden/cfr.npz) bit-exact, the batched mode vs the CPU oracle, and the reference's own
+agent tests (tests/agents/test_cfr.py) restated."""
+import numpy as np
+import pytest
+
+import golden_replay as gr
+from rlcard_amd import seeding
+
+torch = pytest.importorskip('torch')
+
+
+def test_infoset_index_round_trip():
+    from rlcard_amd.agents.cfr_agent import infoset_obs, obs_infoset, NUM_INFOSETS
+    import oracle_lib
+    for i in range(NUM_INFOSETS):
+        o = infoset_obs(i)
+        assert obs_infoset(o) == i
+        assert oracle_lib.cfr_infoset(o.astype(np.uint8)) == i
+    assert obs_infoset(np.array([1., 1., 0., 0., 0., 0.])) == -1
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail('GPU tests need a visible GPU (run them on the MI355X box)')
+
+
+def _check_dicts(agent, d, r):
+    from rlcard_amd.agents.cfr_agent import obs_infoset
+    for name in ('policy', 'average_policy', 'regrets'):
+        got = getattr(agent, name)
+        obs, val = d['r%d_%s_obs' % (r, name)], d['r%d_%s_val' % (r, name)]
+        exp = {obs_infoset(o.astype(np.float64)): v for o, v in zip(obs, val)}
+        got_idx = {obs_infoset(np.frombuffer(k, dtype=np.float64)): v for k, v in got.items()}
+        assert set(got_idx) == set(exp), (r, name)
+        for k, v in exp.items():
+            assert np.array_equal(got_idx[k], v), (r, name, k, got_idx[k], v)
+
+
+@pytest.mark.gpu
+def test_cfr_agent_matches_reference_agent():
+    """The reference CFRAgent on leduc-holdem (seed s, allow_step_back) after K train() calls, bit-exact."""
+    _need_gpu()
+    import rlcard_amd
+    from rlcard_amd.agents import CFRAgent
+    d = gr.load('cfr')
+    for r, (seed, iters) in enumerate(zip(d['seeds'], d['iterations'])):
+        env = rlcard_amd.make('leduc-holdem', config={'seed': int(seed), 'allow_step_back': True})
+        agent = CFRAgent(env)
+        if r == 0:
+            for _ in range(int(iters)):
+                agent.train()
+        else:
+            agent.train(int(iters))      # many iterations per call: same result
+        assert agent.iteration == int(iters)
+        _check_dicts(agent, d, r)
+        # the env is left at the root of the last deal and plays on
+        state, player = env.reset()
+        assert not env.is_over() and len(state['legal_actions']) > 0
+
+
+@pytest.mark.gpu
+def test_cfr_batched_deals_match_oracle(oracle):
+    """B envs = B deals per player per iteration: tables vs the oracle's (players outer, envs inner); fp64 atomics
+    reorder the sums, so values match to 1e-9 relative; keys, and every env's RNG position, match exactly."""
+    _need_gpu()
+    from rlcard_amd import VecEnv
+    from rlcard_amd.agents import CFRAgent
+    B, K = 300, 6
+    v = VecEnv('leduc-holdem', B, seed=11)
+    agent = CFRAgent(v)
+    agent.train(K)
+    torch.cuda.synchronize()
+    keys, lens = seeding.seed_keys(range(11, 11 + B))
+    c = oracle.CFR(keys, lens)
+    c.train(K)
+    t = c.tables()
+    host = agent._tables()
+    assert np.array_equal(host['flags'].astype(np.uint8), t['flags'])
+    for name, bit in (('policy', 1), ('average_policy', 2), ('regrets', 2)):
+        rows = (t['flags'] & bit) != 0          # keys of the dict (unkeyed rows hold the tables' initial values)
+        assert rows.sum() > 50
+        np.testing.assert_allclose(host[name][rows], t[name][rows], rtol=1e-9, atol=1e-9 * np.abs(t[name]).max(),
+                                   err_msg=name)
+    for i in (0, 1, B // 2, B - 1):
+        assert v.rng_position(i) == c.draws(i) % 1248
+
+
+@pytest.mark.gpu
+def test_reference_agent_tests(tmp_path):
+    """tests/agents/test_cfr.py of the reference: eval_step on an unknown obs picks a legal id; save / load keep the
+    dict sizes and the iteration."""
+    _need_gpu()
+    import rlcard_amd
+    from rlcard_amd.agents import CFRAgent
+    env = rlcard_amd.make('leduc-holdem', config={'allow_step_back': True})
+    agent = CFRAgent(env, model_path=str(tmp_path / 'cfr_model'))
+    agent.train(100)
+    agent.save()
+    new_agent = CFRAgent(env, model_path=str(tmp_path / 'cfr_model'))
+    new_agent.load()
+    assert len(agent.policy) == len(new_agent.policy)
+    assert len(agent.average_policy) == len(new_agent.average_policy)
+    assert len(agent.regrets) == len(new_agent.regrets)
+    assert agent.iteration == new_agent.iteration
+    state = {'obs': np.array([1., 1., 0., 0., 0., 0.]), 'legal_actions': {0: None, 2: None},
+             'raw_legal_actions': ['call', 'fold']}
+    action, info = agent.eval_step(state)
+    assert action in [0, 2] and set(info['probs']) == {'call', 'fold'}
+    # eval_step on real states draws from the average policy over the legal ids
+    state, player = env.reset()
+    for _ in range(20):
+        a, info = agent.eval_step(state)
+        assert a in state['legal_actions']
