@@ -28,6 +28,7 @@ template <int NP>
 struct Blackjack {
     static constexpr int OBS = 2, A = 2, P = NP, LB = 1, WORDS = 32, ACTION_BYTES = 1;
     static constexpr int NB = 1;               // raw obs dwords
+    static constexpr bool RING = true;          // MT stream as the byte ring (cs_ring.h)
     static constexpr bool RAW_OBS = true;      // observe() returns byte values, not a 0/1 bitmap
     static constexpr int SCRATCH_WORDS = WORDS;
     // MT staging (see MtLaneT)

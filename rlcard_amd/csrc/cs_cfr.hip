@@ -13,6 +13,7 @@
 // player per iteration, the reference agent) is bit-exact; with more envs the table updates are fp64 atomics
 // (summation order varies run to run).
 #include "cs_device.h"
+#include "cs_ring.h"
 #include "cs_engine.h"
 #include "cs_leduc.h"
 
@@ -112,8 +113,8 @@ __device__ void traverse(const Leduc& root, int player, double iteration, const 
     Frame S[MAXD];
     int d = 0;
     enter(S[0], root, 1.0, 1.0, t);
-    MtLane none;   // Leduc::step draws nothing
-    none.init(nullptr, 0, 0);
+    RingLane<> none;   // Leduc::step draws nothing
+    none.init(nullptr, 2u << 12);
     while (true) {
         Frame& f = S[d];
         const uint32_t rem = f.legal & ~((1u << f.next) - 1u);
@@ -151,24 +152,20 @@ __global__ __launch_bounds__(256) void k_cfr_iteration(uint32_t* mt, uint32_t* c
     const int64_t env = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = env < n;
     const bool atomic = n > 1;
-    MtLane m;
-    if (valid) {
-        const uint32_t w = ctl[env];
-        m.init(mt + env * MT_WORDS, w & 0x7ffu, (w >> 16) & 1u);
-    } else {
-        m.init(mt, 0, 0);
-    }
+    RingLane<> m;
+    if (valid) m.init(mt + env * MT_WORDS, ctl[env]);
+    else m.init(mt, 2u << 12);   // never needs a refill
     Leduc g;
     g.blank();
     if (valid) g.load(st, n, env);
     for (int p = 0; p < 2; p++) {
         if (valid) g.reset(m);          // env.reset(): a new deal from the env's own stream
-        mt_refill_wave(m, lane);        // all 64 lanes
+        ring_refill_wave(m, lane);      // all 64 lanes
         if (valid) traverse(g, p, iteration, t, atomic);
     }
     if (valid) {
         g.store(st, n, env);            // the env is left at the last deal's root (every step stepped back)
-        ctl[env] = m.pos | (m.stale << 16);
+        ctl[env] = m.ctl_word();
     }
 }
 

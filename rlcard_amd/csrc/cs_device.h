@@ -323,7 +323,7 @@ struct Stage {
     static_assert(PAD % 4 == 0, "rows are written as dwords");
     static constexpr int STRIDE = W + PAD;
     static constexpr int CHUNK = STRIDE % 16 == 0 ? 16 : (STRIDE % 8 == 0 ? 8 : 4);   // bytes per persist copy
-    static constexpr int BYTES = ROWS * STRIDE;
+    static constexpr int BYTES = ROWS * STRIDE + 16;   // + 16: Leduc's reset reads a 20-B window at any row offset
 };
 
 __device__ __forceinline__ void wave_sync_lds()
@@ -464,6 +464,14 @@ struct PolicyRng {
 };
 
 // uniform pick among the set bits of a <= 64-action legal mask (k = floor(r * count / 2^32), k-th set bit)
+__device__ __forceinline__ int pick_legal32(uint32_t legal, uint32_t r)
+{
+    const int count = __popc(legal);
+    if (count == 0) return -1;
+    int k = (int)__umulhi(r, (uint32_t)count);
+    while (k--) legal &= legal - 1;
+    return __builtin_ctz(legal);
+}
 __device__ __forceinline__ int pick_legal(uint64_t legal, uint32_t r)
 {
     const int count = __popcll(legal);
@@ -486,9 +494,11 @@ struct RowWriter {
     static constexpr int NB = (ROW + 31) / 32;
     static constexpr int Q = (ROWS * DW) / 4;     // 16-B pieces in a full span
 
+    // 4 bits -> 4 bytes of 0/1: x * (1 + 2^7 + 2^14 + 2^21) puts bit i at bit 8i and the four shifted copies of a
+    // 4-bit x never overlap (bits 0-3, 7-10, 14-17, 21-24), so one 24-bit multiply + mask does it
     __device__ static __forceinline__ uint32_t expand4(uint32_t x)
     {
-        return (x & 1u) | ((x & 2u) << 7) | ((x & 4u) << 14) | ((x & 8u) << 21);
+        return __umul24(x & 15u, 0x204081u) & 0x01010101u;
     }
 
     // bits: NB words of a one-bit-per-byte bitmap; out_span: first byte of the wave's 64 rows; nvalid rows written.

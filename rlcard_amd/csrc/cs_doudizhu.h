@@ -62,6 +62,7 @@ enum { W_HAND = 0, W_PLAYED = 6, W_HIST = 12, W_NTRACE = 17, W_GREATER = 18, W_C
 // reset/step deals.
 struct SeedView {
     static constexpr int SCRATCH_WORDS = 0;
+    static constexpr bool RING = false;   // doudizhu keeps the two-block word layout (cs_doudizhu.hip)
     template <class Prm>
     __host__ __device__ void bind(uint32_t*, const Prm&) {}
     __host__ __device__ void blank() {}

@@ -5,6 +5,7 @@
 //   auto-reset -> wave-cooperative MT19937 refill at the step boundary -> store state.
 // Integer/branchy work: no MFMA. The bound is HBM (obs/legal/reward rows out, packed state + RNG words in/out).
 #include "cs_device.h"
+#include "cs_ring.h"
 #include "cs_engine.h"
 #include "cs_leduc.h"
 #include "cs_limit.h"
@@ -69,23 +70,21 @@ __device__ __forceinline__ LaneCtx lane_ctx(int64_t n)
     return c;
 }
 
+// the lane-per-env games draw from the byte ring (cs_ring.h); invalid lanes get a ring that never needs a refill
 template <int MODE = STAGE_NONE>
-__device__ __forceinline__ MtLaneT<MODE> mt_lane(uint32_t* mt, const uint32_t* ctl, const LaneCtx& c)
+__device__ __forceinline__ RingLane<MODE> ring_lane(uint32_t* mt, const uint32_t* ctl, const LaneCtx& c)
 {
-    MtLaneT<MODE> m;
-    if (c.valid) {
-        const uint32_t w = ctl[c.env];
-        m.init(mt + c.env * MT_WORDS, w & 0x7ffu, (w >> 16) & 1u);
-    } else {
-        m.init(mt, 0, 0);
-    }
+    RingLane<MODE> m;
+    if (c.valid) m.init(mt + c.env * MT_WORDS, ctl[c.env]);
+    else m.init(mt, 0u | 2u << 12);
     return m;
 }
 
+// end-of-step refill (flag bit 0: skipped, every block crossing takes the in-lane serial path -- a test variant)
 template <class G, class M>
 __device__ __forceinline__ void refill(M& m, int lane, int flags)
 {
-    if (!(flags & 1)) mt_refill_wave<G::REFILL_K>(m, lane);
+    if (!(flags & 1)) ring_refill_wave(m, lane);
 }
 
 // obs rows: staged + coalesced when the row is a dword multiple, per-lane bytes otherwise
@@ -176,7 +175,7 @@ template <class G, class M>
 __device__ __forceinline__ void restage(M& m, uint8_t* area, int lane, bool valid)
 {
     if constexpr (G::STAGE_MODE == STAGE_LDS)
-        mt_restage_wave<G::STAGE_W, G::STAGE_PAD, G::STAGE_R, G::RESTAGE_B>(m, area, lane, valid);
+        ring_restage_wave<G::STAGE_W, G::STAGE_PAD, G::STAGE_R, G::RESTAGE_B>(m, area, lane, valid);
 }
 template <class G>
 struct Scratch {   // per-lane LDS words of games that keep state in LDS (blackjack); one word per wave otherwise
@@ -203,6 +202,22 @@ __global__ __launch_bounds__(BLOCK) void k_seed(uint32_t* mt, uint32_t* ctl, uin
     const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     const bool valid = i < count;
     const int64_t env = first + i;
+    if constexpr (G::RING) {   // byte ring: S0 = init_by_array(key) in wbuf, blocks 0..2 generated in place
+        if (!valid) return;
+        uint32_t* wbuf = mt + env * MT_WORDS;
+        const int kl = klen[i] == 2 ? 2 : 1;                    // validated on the host; never trust it here
+        mt_init_by_array(wbuf, keys + 2 * i, kl);
+        for (uint32_t b = 0; b < (uint32_t)RING_GEN; b++) {     // numpy's first draws: block 0 = twist(S0)
+            mt_twist_inplace(wbuf);
+            ring_bytes_serial(wbuf, (uint8_t*)(wbuf + MT_N), b);
+        }
+        G g;
+        g.bind(scratch_of<G>(scr[threadIdx.x / WAVE], lane), prm);
+        g.blank();
+        g.store(st, n, env);
+        ctl[env] = 0u | (uint32_t)(RING_GEN - 1) << 12;          // position 0, latest block in slot 2
+        return;
+    }
     MtLane m;
     m.init(mt, 0, 0);
     if (valid) {
@@ -232,7 +247,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, ui
 {
     CS_SMEM(G);
     const LaneCtx c = lane_ctx(n);
-    MtLane m = mt_lane(mt, ctl, c);
+    RingLane<> m = ring_lane(mt, ctl, c);
     G g;
     g.bind(scratch_of<G>(scr[c.wid], c.lane), prm);
     g.blank();
@@ -256,7 +271,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, ui
         }
         if (out.done) ((uint8_t*)out.done)[c.env] = (uint8_t)g.is_over();
         g.store(st, n, c.env);
-        ctl[c.env] = m.pos | (m.stale << 16);
+        ctl[c.env] = m.ctl_word();
     }
 }
 
@@ -267,7 +282,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uin
 {
     CS_SMEM(G);
     const LaneCtx c = lane_ctx(n);
-    MtLane m = mt_lane(mt, ctl, c);
+    RingLane<> m = ring_lane(mt, ctl, c);
     G g;
     g.bind(scratch_of<G>(scr[c.wid], c.lane), prm);
     g.blank();
@@ -296,7 +311,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uin
         if (out.reward) emit_reward<G>((float*)out.reward, c.env, r);
         if (out.done) ((uint8_t*)out.done)[c.env] = (uint8_t)done;
         g.store(st, n, c.env);
-        ctl[c.env] = m.pos | (m.stale << 16);
+        ctl[c.env] = m.ctl_word();
     }
 }
 
@@ -328,7 +343,7 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
     CS_SMEM_ROWS(G, G::EPW);
     __shared__ __attribute__((aligned(16))) uint8_t stage[WAVES_PER_BLOCK][StageBytes<G>::value];
     const LaneCtx c = lane_ctx<G::EPW>(n);
-    MtLaneT<G::STAGE_MODE> m = mt_lane<G::STAGE_MODE>(mt, ctl, c);
+    RingLane<G::STAGE_MODE> m = ring_lane<G::STAGE_MODE>(mt, ctl, c);
     // MT staging needs both blocks valid at every restage, i.e. the cooperative refill (flag bit 0 off);
     // flag bit 1 disables it (one global load per draw) for A/B runs and fallback-path tests
     const bool staged = !(flags & 3);
@@ -370,7 +385,8 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
         const uint64_t lg = g.legal();
         uint32_t bits[G::NB];
         g.observe(p, bits);
-        const int a = pick_legal(lg, pol.at(seed, genv, t0 + (uint64_t)t, t == 0));
+        const uint32_t pr = pol.at(seed, genv, t0 + (uint64_t)t, t == 0);
+        const int a = G::A <= 32 ? pick_legal32((uint32_t)lg, pr) : pick_legal(lg, pr);
 #ifndef CS_PROF_NO_OBS   // profiling builds only (tools: make variant DEFS=-DCS_PROF_NO_OBS): outputs incomplete
         emit_obs<G, G::EPW>(lds[c.wid], bits, obs, rowbase + c.wave_first, flags, c);
 #endif
@@ -417,7 +433,7 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
     }
     if (c.valid) {
         g.store(st, n, c.env);
-        ctl[c.env] = m.pos | (m.stale << 16) | ((uint32_t)keep << 17);
+        ctl[c.env] = m.ctl_word() | ((uint32_t)keep << 17);
         if (keep) sctl[c.env] = m.sp | (m.sn << 16);
     }
 }

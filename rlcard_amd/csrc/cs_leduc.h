@@ -24,6 +24,9 @@
 #ifndef CS_LEDUC_RESET_SCAN
 #define CS_LEDUC_RESET_SCAN 1
 #endif
+#ifndef CS_LEDUC_RESET_SWAR
+#define CS_LEDUC_RESET_SWAR 1
+#endif
 #ifndef CS_LEDUC_MIN_WAVES
 #define CS_LEDUC_MIN_WAVES 6
 #endif
@@ -37,6 +40,7 @@ namespace cs {
 struct Leduc {
     static constexpr int OBS = 36, A = 4, P = 2, LB = 1, WORDS = 2, ACTION_BYTES = 1;
     static constexpr int NB = 2;  // obs bitmap words
+    static constexpr bool RING = true;          // MT stream as the byte ring (cs_ring.h)
     static constexpr bool RAW_OBS = false;
     static constexpr int SCRATCH_WORDS = 0;
     // MT staging (see MtLaneT)
@@ -81,20 +85,84 @@ struct Leduc {
 
     __device__ __forceinline__ void observe(int player, uint32_t (&bits)[NB]) const
     {
-        bits[0] = bits[1] = 0;
         const int my = player ? in1 : in0, hand = player ? h1 : h0;
-        set_bit(bits, hand >> 1);
-        if (rc >= 1) set_bit(bits, (pub >> 1) + 3);
-        set_bit(bits, my + 6);
-        set_bit(bits, in0 + in1 - my + 21);
+        uint64_t b = (1ull << (hand >> 1)) | (1ull << (my + 6)) | (1ull << (in0 + in1 - my + 21));
+        if (rc >= 1) b |= 1ull << ((pub >> 1) + 3);
+        bits[0] = (uint32_t)b;
+        bits[1] = (uint32_t)(b >> 32);
     }
 
     // dealer.py shuffle (intervals 5..1, swap) then randint(0, 2) for the small blind: six random_interval draws as
     // one state machine over the draw bytes (stage q: 0..4 = the swaps, 5 = the blind), so a wave steps every lane
     // through the staged bytes together instead of looping per interval until its slowest lane accepts
+    // The deal depends only on the first three Fisher-Yates draws: j1 fixes position 5 (p0's hand), j2 position 4
+    // (p1's hand), j3 position 3 (the public card); the draws for positions 2 and 1 and the blind's randint only
+    // consume bytes or pick the blind. random_interval on the low byte, per stage: i=5 mask 7 rejects 6,7; i=4 mask 7
+    // rejects 5..7; i=3 mask 3 never rejects; i=2 mask 3 rejects 3; i=1 and the blind (mask 1) never reject. So with
+    // the next 16 staged bytes as 4 dwords, per-byte accept flags for the three rejecting stages are a few SWAR ops
+    // each, and the stage positions are first-set searches: p0 (i=5), p1 (i=4, after p0), p2 = p1 + 1, p3 (i=2, after
+    // p2), p4 = p3 + 1, p5 = p4 + 1 (the blind). false: the staged window does not hold the whole reset (the caller
+    // runs the byte state machine instead).
+    template <class Rng>
+    __device__ __forceinline__ bool reset_swar(Rng& rng)
+    {
+        const uint32_t k0 = rng.staged_offset();
+        const uint32_t avail = k0 < rng.sn ? rng.sn - k0 : 0u, nv = avail < 16u ? avail : 16u;
+        if (nv < 6u) return false;   // also the first reset of a launch, before any row is staged (stg unset)
+        const uint32_t* row = (const uint32_t*)(rng.stg + (k0 & ~3u));
+        uint32_t w[5];
+#pragma unroll
+        for (int i = 0; i < 5; i++) w[i] = row[i];
+        uint32_t m0 = 0, m1 = 0, m3 = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t x = __builtin_amdgcn_alignbyte(w[i + 1], w[i], k0 & 3u);   // staged bytes k0 + 4i ..
+            const uint32_t b1 = x >> 1, b2 = x >> 2;
+            const uint32_t a0 = ~(b1 & b2) & 0x01010101u;          // (b & 7) <= 5
+            const uint32_t a1 = ~(b2 & (b1 | x)) & 0x01010101u;    // (b & 7) <= 4
+            const uint32_t a3 = ~(x & b1) & 0x01010101u;           // (b & 3) <= 2
+            // byte flags (bits 0, 8, 16, 24) -> 4-bit mask: the product's top nibble (no overlapping partial sums)
+            m0 |= ((a0 * 0x10204080u) >> 28) << (4 * i);
+            m1 |= ((a1 * 0x10204080u) >> 28) << (4 * i);
+            m3 |= ((a3 * 0x10204080u) >> 28) << (4 * i);
+        }
+        const uint32_t valid = (1u << nv) - 1u;
+        m0 &= valid;
+        if (!m0) return false;
+        const uint32_t p0 = __builtin_ctz(m0);
+        const uint32_t r1 = m1 & valid & (0xFFFFFFFEu << p0);
+        if (!r1) return false;
+        const uint32_t p1 = __builtin_ctz(r1), p2 = p1 + 1;
+        const uint32_t r3 = m3 & valid & (0xFFFFFFFEu << p2);
+        if (!r3) return false;
+        const uint32_t p5 = __builtin_ctz(r3) + 2;
+        if (p5 >= nv) return false;
+        const uint8_t* b = rng.stg + k0;
+        const uint32_t j1 = b[p0] & 7u, j2 = b[p1] & 7u, j3 = b[p2] & 3u, s = b[p5] & 1u;
+        rng.advance_by(p5 + 1);
+        // deck positions after the swaps (deck[i] = i before): 5 <- j1; 4 <- deck'[j2]; 3 <- deck''[j3]
+        h0 = (int)j1;
+        h1 = j2 == j1 ? 5 : (int)j2;
+        pub = j3 == j2 ? (j1 == 4 ? 5 : 4) : (j3 == j1 ? 5 : (int)j3);
+        deal_blinds((int)s);
+        return true;
+    }
+
+    __device__ __forceinline__ void deal_blinds(int s)
+    {
+        in0 = s == 0 ? 1 : 2;
+        in1 = s == 0 ? 2 : 1;
+        ptr = s;
+        r0 = in0; r1 = in1;
+        hr = 0; nrn = 0; rc = 0; f0 = 0; f1 = 0; over = 0;
+    }
+
     template <class Rng>
     __device__ __forceinline__ void reset(Rng& rng)
     {
+        if constexpr (Rng::kMode == STAGE_LDS && CS_LEDUC_RESET_SWAR) {
+            if (reset_swar(rng)) return;
+        }
         uint32_t deck = 0x543210u;  // nibble i = card at deck position i
         uint32_t q = 0, s = 0;
         auto take = [&](uint32_t b) {
@@ -127,11 +195,7 @@ struct Leduc {
         }
         while (q < 6) take(rng.next8());
         h0 = (deck >> 20) & 15; h1 = (deck >> 16) & 15; pub = (deck >> 12) & 15;
-        in0 = s == 0 ? 1 : 2;
-        in1 = s == 0 ? 2 : 1;
-        ptr = s;
-        r0 = in0; r1 = in1;
-        hr = 0; nrn = 0; rc = 0; f0 = 0; f1 = 0; over = 0;
+        deal_blinds((int)s);
     }
 
     template <class Rng>
@@ -165,7 +229,7 @@ struct Leduc {
             else if (k1 == pr) { w0 = 0; w1 = 1; }
             else { w0 = k0 >= k1; w1 = k1 >= k0; }
         }
-        const float each = (float)(in0 + in1) / (float)(w0 + w1);
+        const float tot = (float)(in0 + in1), each = (w0 & w1) ? tot * 0.5f : tot;   // total / #winners, exact
         r[0] = (w0 ? each - (float)in0 : -(float)in0) * 0.5f;
         r[1] = (w1 ? each - (float)in1 : -(float)in1) * 0.5f;
     }

@@ -151,6 +151,7 @@ __device__ __forceinline__ void holdem_deal2(Rng& rng, uint32_t& holes, uint32_t
 struct Limit {
     static constexpr int OBS = 72, A = 4, P = 2, LB = 1, WORDS = 4, ACTION_BYTES = 1;
     static constexpr int NB = 3;
+    static constexpr bool RING = true;          // MT stream as the byte ring (cs_ring.h)
     static constexpr bool RAW_OBS = false;
     static constexpr int SCRATCH_WORDS = 0;
     // MT staging (see MtLaneT)

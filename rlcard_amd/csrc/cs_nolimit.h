@@ -37,6 +37,7 @@ namespace cs {
 struct Nolimit {
     static constexpr int OBS = 54, A = 5, P = 2, LB = 1, WORDS = 4, ACTION_BYTES = 1;
     static constexpr int NB = 14;               // raw obs bytes, four per word (RowWriterRaw)
+    static constexpr bool RING = true;          // MT stream as the byte ring (cs_ring.h)
     static constexpr bool RAW_OBS = true;
     static constexpr int SCRATCH_WORDS = 0;
     // MT staging and launch shape as limit hold'em (same deal: ~72 draws per game)

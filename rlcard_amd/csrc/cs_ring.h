@@ -1,0 +1,308 @@
+// cs_ring.h -- the per-env MT19937 stream of the lane-per-env games as a ring of tempered low BYTES.
+//
+// Every draw of Leduc / Limit / No-limit Hold'em / Blackjack is numpy's random_interval(max <= 52), which reads only
+// the low 8 bits of a tempered output word (cs_device.h, MtLaneT). So the stream does not need to be kept as words:
+// per env the engine holds
+//   wbuf[624]  u32   the untempered state words of the LATEST generated block L (the only input of the next twist)
+//   ring[4][624] u8  the low bytes of the tempered outputs of blocks L-3 .. L, block b in slot b % 4
+// (1248 u32 per env: the same footprint as two word blocks). A refill twists THREE blocks in a row in registers --
+// L+1, L+2, L+3 -- writes their bytes into the three consumed slots and only the last block's words back to wbuf.
+// Per 1 872 draws that is one 2.5 KB word read + one 2.5 KB word write + 1 872 B of bytes written and later read
+// (~4.7 B per draw) where the word layout moved ~12 B per draw (block read + block write by the refill, and a 4-B word
+// re-read per draw to temper it). Staging (restage into the LDS rows) becomes a byte copy: no tempering, no packing.
+//
+// ctl[env] u32: bits 0..11 = ring position (draws consumed mod 2 496), bits 12..13 = slot of block L, bit 17 = the
+// rollout's staged LDS rows are valid (cs_kernels.hip). A lane needs a refill when it is inside block L; the
+// wave refills at step boundaries (ring_refill_wave); a lane that would step past L inside a step (more than 624
+// draws in one step: only a rejection loop's tail) generates in-lane (ring_gen_serial): slow, never on the fast path,
+// same numbers.
+#pragma once
+#include "cs_device.h"
+
+namespace cs {
+
+constexpr int RING_SLOTS = 4;
+constexpr int RING_GEN = RING_SLOTS - 1;        // blocks generated per refill
+constexpr uint32_t RING = RING_SLOTS * MT_N;    // 2 496 bytes
+
+__device__ __forceinline__ uint32_t shfl(uint32_t v, int src_lane)
+{
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
+}
+
+// numpy's twist (genrand_int32's reload), in place: mt[k] only reads mt[k+1], mt[k+397] (not yet rewritten) and the
+// already-new mt[k-227]
+__device__ inline void mt_twist_inplace(uint32_t* mt)
+{
+    for (int k = 0; k < MT_N - MT_M; k++) mt[k] = mt_mix(mt[k], mt[k + 1], mt[k + MT_M]);
+    for (int k = MT_N - MT_M; k < MT_N - 1; k++) mt[k] = mt_mix(mt[k], mt[k + 1], mt[k + MT_M - MT_N]);
+    mt[MT_N - 1] = mt_mix(mt[MT_N - 1], mt[0], mt[MT_M - 1]);
+}
+
+// bytes of one block (low byte of every tempered word) into ring slot `slot`, one lane
+__device__ inline void ring_bytes_serial(const uint32_t* w, uint8_t* ring, uint32_t slot)
+{
+    uint32_t* dst = (uint32_t*)(ring + slot * MT_N);
+    for (int i = 0; i < MT_N / 4; i++) {
+        const uint32_t* q = w + 4 * i;
+        dst[i] = (mt_temper(q[0]) & 255u) | (mt_temper(q[1]) & 255u) << 8 | (mt_temper(q[2]) & 255u) << 16 |
+                 (mt_temper(q[3]) & 255u) << 24;
+    }
+}
+
+// one lane generates blocks L+1..L+3 after L (slot lat): the rare in-step path and seeding
+__device__ __attribute__((noinline)) void ring_gen_serial(uint32_t* wbuf, uint32_t lat)
+{
+    uint8_t* ring = (uint8_t*)(wbuf + MT_N);
+    for (uint32_t b = 1; b <= (uint32_t)RING_GEN; b++) {
+        mt_twist_inplace(wbuf);
+        ring_bytes_serial(wbuf, ring, (lat + b) & 3u);
+    }
+}
+
+// Block words in registers, word k = 64c + lane in o[c] (c = 9 holds words 576..623 in lanes 0..47). One twist:
+//   new[k] = mix(old[k], old[k+1] | new[0] (k = 623), old[k+397] (k < 227) | new[k-227])
+// with the cross-lane operands fetched by ds_bpermute; n[c] only depends on n[c-4], n[c-3] and n[0] (computed first).
+__device__ __forceinline__ void twist_regs(const uint32_t (&o)[10], uint32_t (&n)[10], int lane)
+{
+    const int l1 = (lane + 1) & 63, l13 = (lane + 13) & 63, l29 = (lane + 29) & 63;
+#pragma unroll
+    for (int c = 0; c < 10; c++) {
+        uint32_t nxt = shfl(o[c], l1);
+        if (c < 9) {
+            const uint32_t wrap = __builtin_amdgcn_readlane(o[c + 1], 0);
+            nxt = lane == 63 ? wrap : nxt;
+        } else {
+            const uint32_t n0 = __builtin_amdgcn_readlane(n[0], 0);
+            nxt = lane == 47 ? n0 : nxt;
+        }
+        uint32_t far_old = 0, far_new = 0;
+        if (c <= 3) {                                        // k + 397 = 64 (c + 6) + lane + 13
+            const uint32_t x6 = shfl(o[c + 6], l13);
+            const uint32_t x7 = c + 7 <= 9 ? shfl(o[c + 7 <= 9 ? c + 7 : 9], l13) : 0u;
+            far_old = lane < 51 ? x6 : x7;
+        }
+        if (c >= 3) {                                        // k - 227 = 64 (c - 4) + lane + 29
+            const uint32_t y3 = shfl(n[c - 3], l29);
+            const uint32_t y4 = c >= 4 ? shfl(n[c >= 4 ? c - 4 : 0], l29) : 0u;
+            far_new = lane < 35 ? y4 : y3;
+        }
+        const int k = 64 * c + lane;
+        const uint32_t far = k < MT_N - MT_M ? far_old : far_new;
+        n[c] = mt_mix(o[c], nxt, far);
+    }
+}
+
+// Wave-cooperative refill of one env: blocks L+1..L+3 from wbuf (block L, slot lat). All 64 lanes must call.
+__device__ __forceinline__ void ring_gen_wave(gu32* wbuf, uint32_t lat, int lane)
+{
+    uint32_t o[10], n[10];
+#pragma unroll
+    for (int c = 0; c < 10; c++) o[c] = (c < 9 || lane < 48) ? wbuf[64 * c + lane] : 0u;
+    gu32* ring = wbuf + MT_N;   // 624 dwords of bytes
+#pragma unroll
+    for (int b = 1; b <= RING_GEN; b++) {
+        twist_regs(o, n, lane);
+        const uint32_t slot = (lat + (uint32_t)b) & 3u;
+#pragma unroll
+        for (int c = 0; c < 10; c++) {
+            const int t = (int)(mt_temper(n[c]) & 255u);
+            const uint32_t t1 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x101, 0xF, 0xF, true);  // row_shl:1
+            const uint32_t t2 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x102, 0xF, 0xF, true);  // row_shl:2
+            const uint32_t t3 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x103, 0xF, 0xF, true);  // row_shl:3
+            if ((lane & 3) == 0 && (c < 9 || lane < 48))
+                ring[slot * (MT_N / 4) + 16 * c + (lane >> 2)] = (uint32_t)t | (t1 << 8) | (t2 << 16) | (t3 << 24);
+            o[c] = n[c];
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 10; c++)
+        if (c < 9 || lane < 48) wbuf[64 * c + lane] = o[c];
+}
+
+// One lane's view of its env's byte ring. MODE as MtLaneT: STAGE_NONE reads the ring in HBM per draw; STAGE_LDS
+// reads the lane's staged LDS row (ring_restage_wave), HBM only past its end.
+template <int MODE = STAGE_NONE>
+struct RingLane {
+    static constexpr int kMode = MODE;
+    uint32_t* base;   // wbuf of the env (mt + env * 1248); the ring bytes follow it
+    uint32_t pos;     // ring position
+    uint32_t lat;     // slot of the latest generated block
+    uint32_t sp, sn;  // ring position of staged byte 0; staged bytes
+    const uint8_t* stg;
+
+    __device__ __forceinline__ void init(uint32_t* p_base, uint32_t ctlw)
+    {
+        base = p_base;
+        pos = ctlw & 0xFFFu;
+        lat = (ctlw >> 12) & 3u;
+        sp = 0;
+        sn = 0;
+        stg = nullptr;
+    }
+    __device__ __forceinline__ uint32_t ctl_word() const { return pos | lat << 12; }
+    __device__ __forceinline__ const uint8_t* ring() const { return (const uint8_t*)(base + MT_N); }
+    __device__ __forceinline__ uint32_t limit() const { return ((lat + 1u) & 3u) * (uint32_t)MT_N; }
+    // draws left before the end of the generated data (1 .. RING)
+    __device__ __forceinline__ uint32_t ahead() const
+    {
+        const uint32_t d = limit() + RING - pos;
+        return d > RING ? d - RING : d;
+    }
+    __device__ __forceinline__ bool needs_refill() const { return ahead() <= (uint32_t)MT_N; }   // inside block L
+
+    __device__ __forceinline__ void gen_serial()
+    {
+        ring_gen_serial(base, lat);
+        lat = (lat + (uint32_t)RING_GEN) & 3u;
+    }
+
+    __device__ __forceinline__ void advance()
+    {
+        pos = pos + 1u == RING ? 0u : pos + 1u;
+        if (pos == limit()) gen_serial();
+    }
+
+    __device__ __forceinline__ uint32_t staged_offset() const { return pos >= sp ? pos - sp : pos + RING - sp; }
+
+    // the ring byte at pos, read as its dword: a byte load here would let the compiler merge it with the staged LDS
+    // byte load into one load through a select of pointers of two address spaces (clang crashes on that)
+    __device__ __forceinline__ uint32_t ring_byte() const
+    {
+        return (((const uint32_t*)ring())[pos >> 2] >> (8 * (pos & 3u))) & 255u;
+    }
+
+    // low 8 bits of the next tempered word
+    __device__ __forceinline__ uint32_t next8()
+    {
+        uint32_t v;
+        if constexpr (MODE == STAGE_NONE) {
+            v = ring_byte();
+        } else {
+            const uint32_t k = staged_offset();
+            if (k < sn) v = stg[k];
+            else v = ring_byte();
+        }
+        advance();
+        return v;
+    }
+
+    // numpy random_interval(max) for max <= 255: smallest all-ones mask >= max, reject while (byte & mask) > max
+    __device__ __forceinline__ uint32_t interval(uint32_t max)
+    {
+        if (max == 0) return 0;
+        uint32_t mask = max;
+        mask |= mask >> 1;
+        mask |= mask >> 2;
+        mask |= mask >> 4;
+        uint32_t v;
+        do {
+            v = next8() & mask;
+        } while (v > max);
+        return v;
+    }
+
+    // pos += n (n < 624)
+    __device__ __forceinline__ void advance_by(uint32_t n)
+    {
+        const uint32_t a = ahead();
+        uint32_t np = pos + n;
+        if (np >= RING) np -= RING;
+        if (n >= a) gen_serial();
+        pos = np;
+    }
+
+    // random_interval(i) for i = hi .. 1 with every result discarded: the staged bytes scanned branch-free (see
+    // MtLaneT::skip_intervals), then the ring
+    __device__ __forceinline__ void skip_intervals(uint32_t hi)
+    {
+        uint32_t i = hi;
+        if constexpr (MODE == STAGE_LDS) {
+            const uint32_t k0 = staged_offset();
+            uint32_t k = k0;
+            while (i != 0 && k < sn) {
+                const uint32_t sh = k & 3u;
+                const uint32_t w = *(const uint32_t*)(stg + (k - sh)) >> (8 * sh);
+#pragma unroll
+                for (uint32_t t = 0; t < 4; t++) {
+                    if (t < 4 - sh && i != 0 && k < sn) {
+                        const uint32_t u = (w >> (8 * t)) & (0xFFFFFFFFu >> __builtin_clz(i));
+                        i -= u <= i ? 1u : 0u;
+                        k++;
+                    }
+                }
+            }
+            advance_by(k - k0);
+        }
+        for (; i >= 1; i--) (void)interval(i);
+    }
+};
+
+// End-of-step convergence point: the wave refills every lane that is inside its latest block. All 64 lanes call.
+template <class M>
+__device__ __forceinline__ void ring_refill_wave(M& m, int lane)
+{
+    uint64_t need = __ballot(m.needs_refill());
+    while (need) {
+        const int j = __builtin_ctzll(need);
+        need &= need - 1;
+        ring_gen_wave(lane_ptr(m.base, j), __builtin_amdgcn_readlane(m.lat, j), lane);
+        if (lane == j) m.lat = (m.lat + (uint32_t)RING_GEN) & 3u;
+    }
+    // the ring bytes are read later by their owner lane of this same wave: order the stores before those loads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// STAGE_LDS restage, after ring_refill_wave: every lane with fewer than R staged bytes left gets the W ring bytes from
+// its position rounded down to a dword (the refill left >= 624 generated bytes ahead of every lane). W / 4 lanes copy
+// one lane's row with dword loads (the ring is a multiple of 4 bytes, so no dword straddles its end); 64 / (W / 4)
+// rows per load instruction, B instructions in flight per pass. All 64 lanes must call.
+template <int W, int PAD, int R, int B>
+__device__ __forceinline__ void ring_restage_wave(RingLane<STAGE_LDS>& m, uint8_t* area, int lane, bool valid)
+{
+    constexpr int STRIDE = Stage<W, PAD>::STRIDE, DW = W / 4, RPI = WAVE / DW;
+    static_assert(DW <= WAVE && WAVE % DW == 0, "a staged row is copied by W / 4 lanes");
+    m.stg = area + lane * STRIDE;
+    const uint32_t k = m.staged_offset();
+    uint64_t todo = __ballot(valid && (k >= m.sn || m.sn - k < (uint32_t)R));
+    const int row = lane / DW, col = lane - row * DW;
+    const uint32_t rbase_lo = (uint32_t)(uintptr_t)m.ring(), rbase_hi = (uint32_t)((uintptr_t)m.ring() >> 32);
+    const uint32_t p4 = m.pos & ~3u;
+    while (todo) {
+        int js[B * RPI];
+        js[0] = __builtin_ctzll(todo);
+        todo &= todo - 1;
+#pragma unroll
+        for (int q = 1; q < B * RPI; q++) {
+            js[q] = todo ? __builtin_ctzll(todo) : js[0];   // fewer left: repeat the first (same bytes, harmless)
+            todo &= todo - 1;
+        }
+        uint32_t v[B];
+        int src[B];
+#pragma unroll
+        for (int b = 0; b < B; b++) {
+            int s = js[b * RPI];
+#pragma unroll
+            for (int r = 1; r < RPI; r++) s = row == r ? js[b * RPI + r] : s;
+            src[b] = s;
+            const uint64_t rb = (uint64_t)shfl(rbase_lo, s) | (uint64_t)shfl(rbase_hi, s) << 32;
+            uint32_t off = shfl(p4, s) + 4u * (uint32_t)col;
+            if (off >= RING) off -= RING;
+            const gu32* rp = (const gu32*)(uintptr_t)rb;
+            v[b] = rp[off >> 2];
+        }
+#pragma unroll
+        for (int b = 0; b < B; b++) *(uint32_t*)(area + src[b] * STRIDE + 4 * col) = v[b];
+#pragma unroll
+        for (int q = 0; q < B * RPI; q++) {
+            if (lane == js[q]) {
+                m.sp = p4;
+                m.sn = W;
+            }
+        }
+    }
+    wave_sync_lds();
+}
+
+}  // namespace cs

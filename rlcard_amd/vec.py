@@ -206,10 +206,17 @@ class VecEnv:
         buf = (C.c_uint32 * self.info.state_words)(*[int(w) & 0xFFFFFFFF for w in words])
         _abi.check(_abi.lib().cs_set_env_state(self._h, int(env), buf, self.info.state_words), 'cs_set_env_state')
 
+    @property
+    def rng_period(self):
+        """Draws after which the stream position wraps: the byte ring of the lane-per-env games holds 4 blocks
+        (rlcard_amd/csrc/cs_ring.h), doudizhu's word layout 2."""
+        return 1248 if self.env_id == 'doudizhu' else 2496
+
     def rng_position(self, env):
+        """Draws consumed by env `env`, modulo rng_period."""
         v = C.c_uint32()
         _abi.check(_abi.lib().cs_get_rng_ctl(self._h, int(env), C.byref(v)), 'cs_get_rng_ctl')
-        return v.value & 0x7FF
+        return v.value & (0x7FF if self.env_id == 'doudizhu' else 0xFFF)
 
     def set_kernel_flags(self, flags):
         _abi.check(_abi.lib().cs_debug_set_kernel_flags(self._h, int(flags)), 'cs_debug_set_kernel_flags')
