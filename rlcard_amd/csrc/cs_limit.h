@@ -143,7 +143,11 @@ __device__ __forceinline__ void holdem_deal2(Rng& rng, uint32_t& holes, uint32_t
         if (k < 4) d0 |= vj << F0[k < 4 ? k : 0];
         else d1 |= vj << (6 * (k - 4));
     }
+#ifdef CS_PROF_NO_SKIP   // profiling builds only: wrong streams, timing of the skip scan
+    rng.advance_by(60u);
+#else
     rng.skip_intervals(42u);   // deck positions 42..1 are never dealt: only the words they consume matter
+#endif
     holes = d0;
     board = d1;
 }

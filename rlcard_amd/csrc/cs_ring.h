@@ -212,27 +212,33 @@ struct RingLane {
         pos = np;
     }
 
-    // random_interval(i) for i = hi .. 1 with every result discarded: the staged bytes scanned branch-free (see
-    // MtLaneT::skip_intervals), then the ring
+    // random_interval(i) for i = hi .. 1 with every result discarded: only how many bytes the draws consume matters.
+    // The staged bytes are read as whole dwords at any byte offset (alignbyte of two aligned dwords) and scanned
+    // branch-free -- per byte: the mask width of i, a bit-field extract, one compare -- for the draws i = hi .. 2; the
+    // last draw (mask 1) always takes exactly one byte. A lane that runs out of staged bytes finishes through interval().
     __device__ __forceinline__ void skip_intervals(uint32_t hi)
     {
         uint32_t i = hi;
         if constexpr (MODE == STAGE_LDS) {
             const uint32_t k0 = staged_offset();
-            uint32_t k = k0;
-            while (i != 0 && k < sn) {
-                const uint32_t sh = k & 3u;
-                const uint32_t w = *(const uint32_t*)(stg + (k - sh)) >> (8 * sh);
+            if (i >= 2 && k0 < sn) {
+                const uint32_t* row = (const uint32_t*)(stg + (k0 & ~3u));
+                const uint32_t sh = k0 & 3u, nd = (sn - k0) >> 2;   // whole dwords staged from k0
+                uint32_t cnt = 0, lo = row[0];
+                for (uint32_t d = 0; d < nd && i >= 2; d++) {
+                    const uint32_t hw = row[d + 1];
+                    const uint32_t x = __builtin_amdgcn_alignbyte(hw, lo, sh);
+                    lo = hw;
 #pragma unroll
-                for (uint32_t t = 0; t < 4; t++) {
-                    if (t < 4 - sh && i != 0 && k < sn) {
-                        const uint32_t u = (w >> (8 * t)) & (0xFFFFFFFFu >> __builtin_clz(i));
-                        i -= u <= i ? 1u : 0u;
-                        k++;
+                    for (uint32_t t = 0; t < 4; t++) {
+                        const bool live = i >= 2;
+                        const uint32_t u = __builtin_amdgcn_ubfe(x, 8 * t, 32u - __builtin_clz(i));
+                        cnt += live ? 1u : 0u;
+                        i -= (live && u <= i) ? 1u : 0u;
                     }
                 }
+                advance_by(cnt);
             }
-            advance_by(k - k0);
         }
         for (; i >= 1; i--) (void)interval(i);
     }
@@ -257,49 +263,48 @@ __device__ __forceinline__ void ring_refill_wave(M& m, int lane)
 // STAGE_LDS restage, after ring_refill_wave: every lane with fewer than R staged bytes left gets the W ring bytes from
 // its position rounded down to a dword (the refill left >= 624 generated bytes ahead of every lane). W / 4 lanes copy
 // one lane's row with dword loads (the ring is a multiple of 4 bytes, so no dword straddles its end); 64 / (W / 4)
-// rows per load instruction, B instructions in flight per pass. All 64 lanes must call.
+// rows per load instruction, B instructions in flight per pass. The needy lanes are ranked with mbcnt and a ds_permute
+// pushes each one's id to the lane of its rank, so a pass picks its rows with one bpermute (no scalar bit-scan loops).
+// All 64 lanes must call.
 template <int W, int PAD, int R, int B>
 __device__ __forceinline__ void ring_restage_wave(RingLane<STAGE_LDS>& m, uint8_t* area, int lane, bool valid)
 {
-    constexpr int STRIDE = Stage<W, PAD>::STRIDE, DW = W / 4, RPI = WAVE / DW;
+    constexpr int STRIDE = Stage<W, PAD>::STRIDE, DW = W / 4, RPI = WAVE / DW, PER = B * RPI;
     static_assert(DW <= WAVE && WAVE % DW == 0, "a staged row is copied by W / 4 lanes");
     m.stg = area + lane * STRIDE;
     const uint32_t k = m.staged_offset();
-    uint64_t todo = __ballot(valid && (k >= m.sn || m.sn - k < (uint32_t)R));
-    const int row = lane / DW, col = lane - row * DW;
-    const uint32_t rbase_lo = (uint32_t)(uintptr_t)m.ring(), rbase_hi = (uint32_t)((uintptr_t)m.ring() >> 32);
-    const uint32_t p4 = m.pos & ~3u;
-    while (todo) {
-        int js[B * RPI];
-        js[0] = __builtin_ctzll(todo);
-        todo &= todo - 1;
+    const bool needy = valid && (k >= m.sn || m.sn - k < (uint32_t)R);
+    const uint64_t todo = __ballot(needy);
+    if (todo) {
+        const int count = __popcll(todo);
+        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(todo >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)todo, 0u));
+        // a full permutation: needy lanes to their rank, the others after them
+        const int dst = needy ? rank : count + (lane - rank);
+        const int who = __builtin_amdgcn_ds_permute(dst << 2, lane);   // lane q < count: the q-th needy lane
+        const int row = lane / DW, col = lane - row * DW;
+        const uint32_t rbase_lo = (uint32_t)(uintptr_t)m.ring(), rbase_hi = (uint32_t)((uintptr_t)m.ring() >> 32);
+        const uint32_t p4 = m.pos & ~3u;
+        for (int base = 0; base < count; base += PER) {
+            uint32_t v[B];
+            int src[B];
 #pragma unroll
-        for (int q = 1; q < B * RPI; q++) {
-            js[q] = todo ? __builtin_ctzll(todo) : js[0];   // fewer left: repeat the first (same bytes, harmless)
-            todo &= todo - 1;
-        }
-        uint32_t v[B];
-        int src[B];
-#pragma unroll
-        for (int b = 0; b < B; b++) {
-            int s = js[b * RPI];
-#pragma unroll
-            for (int r = 1; r < RPI; r++) s = row == r ? js[b * RPI + r] : s;
-            src[b] = s;
-            const uint64_t rb = (uint64_t)shfl(rbase_lo, s) | (uint64_t)shfl(rbase_hi, s) << 32;
-            uint32_t off = shfl(p4, s) + 4u * (uint32_t)col;
-            if (off >= RING) off -= RING;
-            const gu32* rp = (const gu32*)(uintptr_t)rb;
-            v[b] = rp[off >> 2];
-        }
-#pragma unroll
-        for (int b = 0; b < B; b++) *(uint32_t*)(area + src[b] * STRIDE + 4 * col) = v[b];
-#pragma unroll
-        for (int q = 0; q < B * RPI; q++) {
-            if (lane == js[q]) {
-                m.sp = p4;
-                m.sn = W;
+            for (int b = 0; b < B; b++) {
+                const int q = base + b * RPI + row;
+                const int s = (int)shfl((uint32_t)who, q < count ? q : base);   // past the end: repeat (harmless)
+                src[b] = s;
+                const uint64_t rb = (uint64_t)shfl(rbase_lo, s) | (uint64_t)shfl(rbase_hi, s) << 32;
+                uint32_t off = shfl(p4, s) + 4u * (uint32_t)col;
+                if (off >= RING) off -= RING;
+                const gu32* rp = (const gu32*)(uintptr_t)rb;
+                v[b] = rp[off >> 2];
             }
+#pragma unroll
+            for (int b = 0; b < B; b++) *(uint32_t*)(area + src[b] * STRIDE + 4 * col) = v[b];
+        }
+        if (needy) {
+            m.sp = p4;
+            m.sn = W;
         }
     }
     wave_sync_lds();
