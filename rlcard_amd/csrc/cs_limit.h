@@ -116,6 +116,45 @@ __device__ inline uint32_t holdem_rank7(uint64_t cnt, uint64_t smp)
     return cat << 20 | v0 << 16 | v1 << 12 | v2 << 8 | v3 << 4 | v4;
 }
 
+// The nine dealt draws (random_interval(i), i = 51..43, mask 63) from the staged bytes without rejection loops: one
+// branch-free pass over the next 24 staged bytes (bit-field extract, compare with the current i) marks the accepted
+// bytes in a 24-bit mask, then the k-th set bit's byte is draw k. false: fewer than 28 staged bytes, or fewer than nine
+// acceptances among the 24 (the caller draws with interval(), same numbers).
+template <class Rng>
+__device__ __forceinline__ bool deal9_staged(Rng& rng, uint32_t (&j)[9])
+{
+    const uint32_t k0 = rng.staged_offset();
+    if (k0 >= rng.sn || rng.sn - k0 < 28u) return false;
+    const uint32_t* row = (const uint32_t*)(rng.stg + (k0 & ~3u));
+    const uint32_t sh = k0 & 3u;
+    uint32_t w[7];
+#pragma unroll
+    for (int q = 0; q < 7; q++) w[q] = row[q];
+    uint32_t i = 51, acc_mask = 0, n = 0;
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        const uint32_t x = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh);   // staged bytes k0 + 4q ..
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const bool live = i >= 43u;
+            const uint32_t u = __builtin_amdgcn_ubfe(x, 8 * t, 6);
+            const bool acc = live && u <= i;
+            acc_mask |= acc ? 1u << (4 * q + t) : 0u;
+            i -= acc ? 1u : 0u;
+            n += live ? 1u : 0u;
+        }
+    }
+    if (i >= 43u) return false;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        const uint32_t p = __builtin_ctz(acc_mask);
+        acc_mask &= acc_mask - 1u;
+        j[k] = rng.stg[k0 + p] & 63u;
+    }
+    rng.advance_by(n);
+    return true;
+}
+
 // The hold'em deal (limitholdem/dealer.py: shuffle the 52-card deck, deal_card = pop()) of a heads-up game: hole i ->
 // player i % 2, card i / 2 from deck[51 - i]; flop deck[47..45], turn deck[44], river deck[43]. Fisher-Yates fixes
 // position i at step i, and only deck[43..51] is ever dealt, so the first nine swaps are tracked (swap k writes card vj
@@ -125,12 +164,25 @@ __device__ inline uint32_t holdem_rank7(uint64_t cnt, uint64_t smp)
 template <class Rng>
 __device__ __forceinline__ void holdem_deal2(Rng& rng, uint32_t& holes, uint32_t& board)
 {
+    uint32_t js[9];
+    bool staged = false;
+#ifdef CS_PROF_NO_DEAL9   // profiling builds only: wrong deals, timing of the tracked draws
+#pragma unroll
+    for (int k = 0; k < 9; k++) js[k] = (uint32_t)k;
+    rng.advance_by(12u);
+    staged = true;
+#else
+    if constexpr (Rng::kMode == STAGE_LDS) staged = deal9_staged(rng, js);
+#endif
+    if (!staged) {
+#pragma unroll
+        for (int k = 0; k < 9; k++) js[k] = rng.interval(51u - (uint32_t)k);
+    }
     uint32_t JV[9];
     uint32_t d0 = 0, d1 = 0;
 #pragma unroll
     for (int k = 0; k < 9; k++) {
-        const uint32_t i = 51 - k;
-        const uint32_t j = rng.interval(i);
+        const uint32_t i = 51 - k, j = js[k];
         uint32_t vi = i, vj = j;
 #pragma unroll
         for (int q = 0; q < k; q++) {   // oldest -> newest: the newest write to a position wins
@@ -274,11 +326,15 @@ struct Limit {
             uint64_t c0 = bc, s0 = bs;
             tally_card(hole(0, 0), c0, s0);
             tally_card(hole(0, 1), c0, s0);
+#ifdef CS_PROF_NO_EVAL   // profiling builds only: wrong payoffs, timing of the evaluator
+            const uint32_t v0 = (uint32_t)(c0 ^ s0), v1 = (uint32_t)(bc ^ bs);
+#else
             const uint32_t v0 = holdem_rank7(c0, s0);
             uint64_t c1 = bc, s1 = bs;
             tally_card(hole(1, 0), c1, s1);
             tally_card(hole(1, 1), c1, s1);
             const uint32_t v1 = holdem_rank7(c1, s1);
+#endif
             win0 = v0 >= v1; win1 = v1 >= v0;
         }
         const int a = in0(), b = in1(), m = a < b ? a : b;

@@ -224,8 +224,20 @@ struct RingLane {
             if (i >= 2 && k0 < sn) {
                 const uint32_t* row = (const uint32_t*)(stg + (k0 & ~3u));
                 const uint32_t sh = k0 & 3u, nd = (sn - k0) >> 2;   // whole dwords staged from k0
-                uint32_t cnt = 0, lo = row[0];
-                for (uint32_t d = 0; d < nd && i >= 2; d++) {
+                uint32_t cnt = 0, lo = row[0], d = 0;
+                // while i >= 6 a dword cannot take i below 2: no per-byte liveness
+                for (; d < nd && i >= 6; d++) {
+                    const uint32_t hw = row[d + 1];
+                    const uint32_t x = __builtin_amdgcn_alignbyte(hw, lo, sh);
+                    lo = hw;
+#pragma unroll
+                    for (uint32_t t = 0; t < 4; t++) {
+                        const uint32_t u = __builtin_amdgcn_ubfe(x, 8 * t, 32u - __builtin_clz(i));
+                        i -= u <= i ? 1u : 0u;
+                    }
+                    cnt += 4;
+                }
+                for (; d < nd && i >= 2; d++) {
                     const uint32_t hw = row[d + 1];
                     const uint32_t x = __builtin_amdgcn_alignbyte(hw, lo, sh);
                     lo = hw;
