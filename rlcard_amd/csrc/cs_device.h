@@ -319,7 +319,7 @@ __device__ __forceinline__ void mt_refill_wave(M& m, int lane)
 // persist copies move 16 / 8 / 4 B per lane, whatever the stride allows.
 template <int W, int PAD, int ROWS = WAVE>
 struct Stage {
-    static_assert(W % WAVE == 0, "LDS staging rows are filled 64 words per wave instruction");
+    static_assert(W % 16 == 0 && WAVE % (W / 4) == 0, "a staged row is copied by W / 4 lanes of one wave instruction");
     static_assert(PAD % 4 == 0, "rows are written as dwords");
     static constexpr int STRIDE = W + PAD;
     static constexpr int CHUNK = STRIDE % 16 == 0 ? 16 : (STRIDE % 8 == 0 ? 8 : 4);   // bytes per persist copy

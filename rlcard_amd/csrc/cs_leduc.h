@@ -30,6 +30,9 @@
 #ifndef CS_LEDUC_MIN_WAVES
 #define CS_LEDUC_MIN_WAVES 6
 #endif
+#ifndef CS_LEDUC_STAGE_W
+#define CS_LEDUC_STAGE_W 64
+#endif
 #ifndef CS_LEDUC_STAGE_R
 
 #define CS_LEDUC_STAGE_R 12
@@ -44,7 +47,7 @@ struct Leduc {
     static constexpr bool RAW_OBS = false;
     static constexpr int SCRATCH_WORDS = 0;
     // MT staging (see MtLaneT)
-    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 64, STAGE_PAD = 4, STAGE_R = CS_LEDUC_STAGE_R;
+    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = CS_LEDUC_STAGE_W, STAGE_PAD = 4, STAGE_R = CS_LEDUC_STAGE_R;
     static constexpr int RESTAGE_B = CS_LEDUC_RESTAGE_B;  // lanes restaged per pass (loads in flight): 4 > 8 > 1
     static constexpr int MIN_WAVES = CS_LEDUC_MIN_WAVES;  // rollout waves per SIMD the register budget must allow
     static constexpr int EPW = 64;        // rollout envs per wave (lane_ctx)
