@@ -163,6 +163,12 @@ struct Leduc {
     template <class Rng>
     __device__ __forceinline__ void reset(Rng& rng)
     {
+#ifdef CS_PROF_NO_RESET   // profiling builds only: wrong deals, timing of the reset
+        rng.advance_by(7u);
+        h0 = 0; h1 = 2; pub = 4;
+        deal_blinds((int)(rng.pos & 1u));
+        return;
+#endif
         if constexpr (Rng::kMode == STAGE_LDS && CS_LEDUC_RESET_SWAR) {
             if (reset_swar(rng)) return;
         }
