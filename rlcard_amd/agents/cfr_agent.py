@@ -17,6 +17,7 @@ import torch
 
 from .. import _abi
 from ..envs.env import Env
+from ..utils import remove_illegal
 from ..vec import VecEnv
 
 NUM_INFOSETS = 2700   # ((hand * 4 + public + 1) * 15 + my chips) * 15 + others' chips
@@ -46,17 +47,6 @@ def obs_infoset(obs):
     if len(h) != 1 or len(p) > 1 or len(m) != 1 or len(q) != 1:
         return -1
     return ((int(h[0]) * 4 + (int(p[0]) + 1 if len(p) else 0)) * 15 + int(m[0])) * 15 + int(q[0])
-
-
-def remove_illegal(action_probs, legal_actions):
-    """rlcard/utils/utils.py:181-198."""
-    probs = np.zeros(action_probs.shape[0])
-    probs[legal_actions] = action_probs[legal_actions]
-    if np.sum(probs) == 0:
-        probs[legal_actions] = 1 / len(legal_actions)
-    else:
-        probs /= sum(probs)
-    return probs
 
 
 class CFRAgent(object):
