@@ -26,13 +26,22 @@
 namespace cs {
 namespace ddz {
 
-constexpr int BLOCK = 256;
+#ifndef CS_DDZ_BLOCK
+#define CS_DDZ_BLOCK 256
+#endif
+#ifndef CS_DDZ_MINW
+#define CS_DDZ_MINW 1   // k_rollout: minimum waves per SIMD the register allocation must allow
+#endif
+constexpr int BLOCK = CS_DDZ_BLOCK;
 constexpr int WPB = BLOCK / WAVE;
 constexpr int MASK_PAD = 4;                       // zero dwords on both sides of the mask image
 constexpr int KTH_LANES = 54, KTH_WORDS = 16;     // kth_legal: lane l scans mask dwords [16 l, 16 l + 16)
 constexpr int MASK_WORDS = MASK_PAD + KTH_LANES * KTH_WORDS + MASK_PAD;
 constexpr int NSEG = 20;                          // 54-bit obs blocks (16 used) + zero tail
 constexpr int BV_WORDS = 32;                      // obs bits (912 + 16 front pad) as dwords
+#ifndef CS_PROF_DDZ
+#define CS_PROF_DDZ 0   // profiling only (wrong outputs): 1 skip legal rows, 2 skip obs rows, 4 skip build_obs
+#endif
 
 struct WaveLds {
     uint32_t mask[MASK_WORDS];   // legal bits: id i at bit (i & 31) of mask[MASK_PAD + i / 32]
@@ -518,15 +527,35 @@ __device__ __forceinline__ uint4 expand_bits16(uint32_t x)   // 16 bits -> 16 by
     return o;
 }
 
+// bytes [lo, hi) of an aligned 16-B chunk, lo == 0 or hi == 16 (a row's first or last chunk): at most four
+// naturally aligned stores of 8 / 4 / 2 / 1 bytes instead of 16 predicated byte stores
+__device__ __forceinline__ void store_part(uint8_t* dst, int lo, int hi, const uint4& v)
+{
+    const uint64_t q0 = v.x | ((uint64_t)v.y << 32), q1 = v.z | ((uint64_t)v.w << 32);
+    if (lo == 0) {                       // prefix [0, hi)
+        int p = 0;
+        uint64_t r = q0;
+        if (hi & 8) { *(uint64_t*)dst = q0; p = 8; r = q1; }
+        if (hi & 4) { *(uint32_t*)(dst + p) = (uint32_t)r; p += 4; r >>= 32; }
+        if (hi & 2) { *(uint16_t*)(dst + p) = (uint16_t)r; p += 2; r >>= 16; }
+        if (hi & 1) dst[p] = (uint8_t)r;
+    } else {                             // suffix [lo, 16): its bytes just below p sit at the top of r
+        const int len = 16 - lo;
+        int p = 16;
+        uint64_t r = q1;
+        if (len & 8) { *(uint64_t*)(dst + 8) = q1; p = 8; r = q0; }
+        if (len & 4) { p -= 4; *(uint32_t*)(dst + p) = (uint32_t)(r >> 32); r <<= 32; }
+        if (len & 2) { p -= 2; *(uint16_t*)(dst + p) = (uint16_t)(r >> 48); r <<= 16; }
+        if (len & 1) { p -= 1; dst[p] = (uint8_t)(r >> 56); }
+    }
+}
+
 __device__ __forceinline__ void store_chunk(uint8_t* dst_al, int o, int nbytes, const uint4& v)
 {
     if (o >= 0 && o + 16 <= nbytes) {
         *(uint4*)dst_al = v;
-    } else {
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-            if (o + k >= 0 && o + k < nbytes) dst_al[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    } else {                             // rows are >= 16 bytes: exactly one end of the chunk is cut
+        store_part(dst_al, o < 0 ? -o : 0, nbytes - o < 16 ? nbytes - o : 16, v);
     }
 }
 
@@ -691,7 +720,7 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n
     emit_state(e, (uint32_t)player, tb, tl, lds[c.wid], c.lane, c.env, out);
 }
 
-__global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n, int T,
+__global__ __launch_bounds__(BLOCK, CS_DDZ_MINW) void k_rollout(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n, int T,
                                                     uint64_t seed, uint64_t t0, uint64_t env_base, cs_traj_out out,
                                                     Tab tb)
 {
@@ -707,21 +736,24 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(uint32_t* mt, uint32_t* ctl, 
     WaveMt m = wave_mt(mt, ctl, c.env);
     if (e.over()) deal(e, m, lane);
     const uint64_t genv = env_base + (uint64_t)c.env;
+    uint32_t rr_lane = 0;
     for (int t = 0; t < T; t++) {
         const int64_t row = (int64_t)t * n + c.env;
         zero_mask(L, lane);
         wave_sync_lds();
         const Cand cd = cand_of(e, tb, tl);
         const Legal lg = build_legal(e, cd, tb, tl, L, lane);
-        build_obs(e, e.cur, L, lane);
+        if (!(CS_PROF_DDZ & 4)) build_obs(e, e.cur, L, lane);
         wave_sync_lds();
         const uint32_t count = lg.total + (cd.leading ? 0u : 1u);
-        const uint32_t rr = philox_u32(seed, genv, t0 + (uint64_t)t);
+        // the policy draws of 64 steps at once, one per lane (vector ALU; the scalar unit is the busy one)
+        if ((t & (WAVE - 1)) == 0) rr_lane = philox_u32(seed, genv, t0 + (uint64_t)(t + lane));
+        const uint32_t rr = rl(rr_lane, t & (WAVE - 1));
         const uint32_t a = kth_legal((uint32_t)(((uint64_t)rr * count) >> 32), lg, L, lane);
         if (!cd.leading && lane == 0) L.mask[MASK_PAD + PASS / 32] |= 1u << (PASS & 31);
         wave_sync_lds();
-        write_obs_row(L, (uint8_t*)out.obs + row * OBS, lane);
-        write_legal_row(L, (uint8_t*)out.legal + row * LB, lane);
+        if (!(CS_PROF_DDZ & 2)) write_obs_row(L, (uint8_t*)out.obs + row * OBS, lane);
+        if (!(CS_PROF_DDZ & 1)) write_legal_row(L, (uint8_t*)out.legal + row * LB, lane);
         const uint32_t p = e.cur;
         e.apply(a, tb, lane);
         const bool done = e.over();
