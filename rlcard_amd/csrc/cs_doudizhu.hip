@@ -480,16 +480,13 @@ __device__ __forceinline__ void build_obs(const Env& e, uint32_t self, WaveLds& 
         if (nt >= 1u) ll_c = rl64(e.hcnt, 11 - (int)((nt - 1u) % 3u));
         if (nt > mate) lt_c = rl64(e.hcnt, 11 - (int)((nt - 1u - mate) % 3u));
     }
+    // the block of lane s, selected without branches (the candidates are wave-uniform)
     const int s = lane;
-    uint64_t direct = 0;
-    if (s == 0) direct = e.hand(self);
-    else if (s == 1) direct = e.hand(self == 0 ? 1u : 0u) + e.hand(self == 2 ? 1u : 2u);
-    else if (s == 2) direct = last_c;
-    else if (s <= 11) direct = e.hcnt;
-    else if (s == 12) direct = self == 0 ? e.q2 : e.q0;
-    else if (s == 13) direct = self == 0 ? e.q1 : e.played(mate);
-    else if (s == 14) direct = ll_c;
-    else if (s == 15) direct = lt_c;
+    const uint64_t u1 = e.hand(self == 0 ? 1u : 0u) + e.hand(self == 2 ? 1u : 2u);
+    const uint64_t u12 = self == 0 ? e.q2 : e.q0, u13 = self == 0 ? e.q1 : e.played(mate);
+    const uint64_t direct = keep64(s == 0, e.hand(self)) | keep64(s == 1, u1) | keep64(s == 2, last_c) |
+                            keep64(s >= 3 && s <= 11, e.hcnt) | keep64(s == 12, u12) | keep64(s == 13, u13) |
+                            keep64(s == 14, ll_c) | keep64(s == 15, lt_c);
     if (s < NSEG) L.segv[s] = cards_bits(direct);
     uint32_t p1, p2;
     if (self == 0) {
@@ -506,17 +503,13 @@ __device__ __forceinline__ void build_obs(const Env& e, uint32_t self, WaveLds& 
         const int x0 = lane == 0 ? 0 : 32 * lane - 16;             // first obs bit of this dword (lane 0: see below)
         const int sg = x0 / 54, off = x0 - 54 * sg;
         uint32_t v = (uint32_t)((L.segv[sg] >> off) | (L.segv[sg + 1] << (54 - off)));
-        if (lane == 0) v <<= 16;                                    // dword 0 = 16 pad bits + obs bits 0..15
-        const uint32_t d1 = p1 - (uint32_t)x0, d2 = p2 - (uint32_t)x0;
-        if (lane != 0) {
-            if (d1 < 32u) v |= 1u << d1;
-            if (d2 < 32u) v |= 1u << d2;
-        }
-        L.bv[lane] = v;
+        const uint32_t d1 = p1 - (uint32_t)x0, d2 = p2 - (uint32_t)x0;   // the one-hots are past dword 0
+        L.bv[lane] = lane == 0 ? v << 16                                  // dword 0 = 16 pad bits + obs bits 0..15
+                               : v | keep32(d1 < 32u, 1u << (d1 & 31u)) | keep32(d2 < 32u, 1u << (d2 & 31u));
     }
 }
 
-// ---- row writers: 16-B stores for the chunks fully inside the row, byte stores at its two ends ------------------
+// ---- row writers: 16-B stores for the chunks fully inside a row; its two end chunks in one pass for both rows --
 __device__ __forceinline__ uint4 expand_bits16(uint32_t x)   // 16 bits -> 16 bytes of 0/1
 {
     uint4 o;
@@ -532,7 +525,9 @@ __device__ __forceinline__ uint4 expand_bits16(uint32_t x)   // 16 bits -> 16 by
 __device__ __forceinline__ void store_part(uint8_t* dst, int lo, int hi, const uint4& v)
 {
     const uint64_t q0 = v.x | ((uint64_t)v.y << 32), q1 = v.z | ((uint64_t)v.w << 32);
-    if (lo == 0) {                       // prefix [0, hi)
+    if (lo == 0 && hi == 16) {
+        *(uint4*)dst = v;
+    } else if (lo == 0) {                // prefix [0, hi)
         int p = 0;
         uint64_t r = q0;
         if (hi & 8) { *(uint64_t*)dst = q0; p = 8; r = q1; }
@@ -550,56 +545,47 @@ __device__ __forceinline__ void store_part(uint8_t* dst, int lo, int hi, const u
     }
 }
 
-__device__ __forceinline__ void store_chunk(uint8_t* dst_al, int o, int nbytes, const uint4& v)
+// chunk q of a row misaligned by mis (its first byte is row byte 16 q - mis; bytes before the row are don't-care)
+__device__ __forceinline__ uint4 obs_chunk(const WaveLds& L, int q, int mis)
 {
-    if (o >= 0 && o + 16 <= nbytes) {
-        *(uint4*)dst_al = v;
-    } else {                             // rows are >= 16 bytes: exactly one end of the chunk is cut
-        store_part(dst_al, o < 0 ? -o : 0, nbytes - o < 16 ? nbytes - o : 16, v);
-    }
+    const int bp = 16 * q - mis + 16;                               // bit of L.bv, >= 1
+    const uint64_t two = (uint64_t)L.bv[bp >> 5] | ((uint64_t)L.bv[(bp >> 5) + 1] << 32);
+    return expand_bits16((uint32_t)(two >> (bp & 31)) & 0xFFFFu);
+}
+__device__ __forceinline__ uint4 legal_chunk(const WaveLds& L, int q, int mis)
+{
+    const int sb = 4 * MASK_PAD + 16 * q - mis;                     // byte of L.mask, >= 1
+    const uint32_t* w = L.mask + (sb >> 2);
+    const int sh = sb & 3;                                          // alignbyte(x, y, 0) = y
+    return make_uint4(__builtin_amdgcn_alignbyte(w[1], w[0], sh), __builtin_amdgcn_alignbyte(w[2], w[1], sh),
+                      __builtin_amdgcn_alignbyte(w[3], w[2], sh), __builtin_amdgcn_alignbyte(w[4], w[3], sh));
 }
 
-__device__ __forceinline__ void write_obs_row(const WaveLds& L, uint8_t* row, int lane)
+// the obs row (OBS bytes) and / or the legal row (LB bytes); null rows are skipped
+__device__ __forceinline__ void write_rows(const WaveLds& L, uint8_t* orow, uint8_t* lrow, int lane)
 {
-    const int mis = (int)((uintptr_t)row & 15u);
-    uint8_t* al = row - mis;
-    const int nchunks = (mis + OBS + 15) >> 4;                       // <= 58
-    if (lane < nchunks) {
-        const int o = 16 * lane - mis;                               // row byte of the chunk's first byte
-        const int bp = 16 + o;                                       // >= 1
-        const uint64_t two = (uint64_t)L.bv[bp >> 5] | ((uint64_t)L.bv[(bp >> 5) + 1] << 32);
-        store_chunk(al + 16 * lane, o, OBS, expand_bits16((uint32_t)(two >> (bp & 31)) & 0xFFFFu));
+    if (orow) {
+        const int mis = (int)((uintptr_t)orow & 15u), nchunks = (mis + OBS + 15) >> 4;   // <= 58
+        if (lane >= 1 && lane < nchunks - 1) *(uint4*)(orow - mis + 16 * lane) = obs_chunk(L, lane, mis);
     }
-}
-
-__device__ __forceinline__ void write_legal_row(const WaveLds& L, uint8_t* row, int lane)
-{
-    const int mis = (int)((uintptr_t)row & 15u);
-    uint8_t* al = row - mis;
-    const int nchunks = (mis + LB + 15) >> 4;                        // <= 216
-    const uint8_t* img = (const uint8_t*)L.mask + 4 * MASK_PAD;      // row byte b at img[b]
+    if (lrow) {
+        const int mis = (int)((uintptr_t)lrow & 15u), nchunks = (mis + LB + 15) >> 4;    // <= 216
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int qn = j * WAVE + lane;
-        if (qn < nchunks) {
-            const int o = 16 * qn - mis;
-            const int sb = 4 * MASK_PAD + o;                             // byte offset into L.mask, >= 1
-            const uint32_t* w = L.mask + (sb >> 2);
-            const int sh = sb & 3;
-            uint4 v;
-            if (sh == 0) {
-                v = make_uint4(w[0], w[1], w[2], w[3]);
-            } else {
-                const uint32_t w4 = w[4];
-                v.x = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
-                v.y = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
-                v.z = __builtin_amdgcn_alignbyte(w[3], w[2], sh);
-                v.w = __builtin_amdgcn_alignbyte(w4, w[3], sh);
-            }
-            store_chunk(al + 16 * qn, o, LB, v);
+        for (int j = 0; j < 4; j++) {
+            const int q = j * WAVE + lane;
+            if (q >= 1 && q < nchunks - 1) *(uint4*)(lrow - mis + 16 * q) = legal_chunk(L, q, mis);
         }
     }
-    (void)img;
+    // lanes 0 / 1: the obs row's first / last chunk, lanes 2 / 3: the legal row's
+    const bool is_obs = lane < 2;
+    uint8_t* row = is_obs ? orow : lrow;
+    if (lane < 4 && row) {
+        const int nbytes = is_obs ? OBS : LB;
+        const int mis = (int)((uintptr_t)row & 15u), nchunks = (mis + nbytes + 15) >> 4;
+        const int q = (lane & 1) ? nchunks - 1 : 0, o = 16 * q - mis;
+        const uint4 v = is_obs ? obs_chunk(L, q, mis) : legal_chunk(L, q, mis);
+        store_part(row - mis + 16 * q, o < 0 ? -o : 0, nbytes - o < 16 ? nbytes - o : 16, v);
+    }
 }
 
 struct Ctx {
@@ -638,8 +624,8 @@ __device__ __forceinline__ void emit_state(const Env& e, uint32_t self, const Ta
     if (!e.over() && !cd.leading && lane == 0) L.mask[MASK_PAD + PASS / 32] |= 1u << (PASS & 31);
     build_obs(e, self, L, lane);
     wave_sync_lds();
-    if (out.obs) write_obs_row(L, (uint8_t*)out.obs + row * OBS, lane);
-    if (out.legal) write_legal_row(L, (uint8_t*)out.legal + row * LB, lane);
+    write_rows(L, out.obs ? (uint8_t*)out.obs + row * OBS : nullptr,
+               out.legal ? (uint8_t*)out.legal + row * LB : nullptr, lane);
     if (lane == 0) {
         if (out.player) ((uint8_t*)out.player)[row] = (uint8_t)e.cur;
         if (out.done) ((uint8_t*)out.done)[row] = (uint8_t)e.over();
@@ -752,8 +738,8 @@ __global__ __launch_bounds__(BLOCK, CS_DDZ_MINW) void k_rollout(uint32_t* mt, ui
         const uint32_t a = kth_legal((uint32_t)(((uint64_t)rr * count) >> 32), lg, L, lane);
         if (!cd.leading && lane == 0) L.mask[MASK_PAD + PASS / 32] |= 1u << (PASS & 31);
         wave_sync_lds();
-        if (!(CS_PROF_DDZ & 2)) write_obs_row(L, (uint8_t*)out.obs + row * OBS, lane);
-        if (!(CS_PROF_DDZ & 1)) write_legal_row(L, (uint8_t*)out.legal + row * LB, lane);
+        write_rows(L, (CS_PROF_DDZ & 2) ? nullptr : (uint8_t*)out.obs + row * OBS,
+                   (CS_PROF_DDZ & 1) ? nullptr : (uint8_t*)out.legal + row * LB, lane);
         const uint32_t p = e.cur;
         e.apply(a, tb, lane);
         const bool done = e.over();
@@ -772,7 +758,7 @@ __global__ __launch_bounds__(BLOCK, CS_DDZ_MINW) void k_rollout(uint32_t* mt, ui
                     wave_sync_lds();
                     build_obs(e, q, L, lane);
                     wave_sync_lds();
-                    write_obs_row(L, (uint8_t*)out.final_obs + (row * P + q) * OBS, lane);
+                    write_rows(L, (uint8_t*)out.final_obs + (row * P + q) * OBS, nullptr, lane);
                 }
             }
             deal(e, m, lane);
