@@ -4,6 +4,8 @@
 //   load packed state (word-major SoA, coalesced) -> per step: observe / legal / pick / emit rows / step / payoffs /
 //   auto-reset -> wave-cooperative MT19937 refill at the step boundary -> store state.
 // Integer/branchy work: no MFMA. The bound is HBM (obs/legal/reward rows out, packed state + RNG words in/out).
+#include <type_traits>
+
 #include "cs_device.h"
 #include "cs_ring.h"
 #include "cs_engine.h"
@@ -186,6 +188,57 @@ __device__ __forceinline__ uint32_t* scratch_of(uint32_t* wave_area, int lane)
 {
     return G::SCRATCH_WORDS > 0 ? wave_area + lane : nullptr;
 }
+// ---- hold'em deal queue (cs_limit.h): q = the env's queue words, `stride` apart (state in HBM: n; LDS copy: 1) ------
+template <class G, class = void>
+struct DqOf {
+    static constexpr int value = 0, words = 0;
+};
+template <class G>
+struct DqOf<G, std::void_t<decltype(G::DQ)>> {
+    static constexpr int value = G::DQ, words = G::DQ > 0 ? 1 + 2 * G::DQ : 0;
+};
+
+// draw the env's next deal into its queue (the caller checks for room)
+template <class G, class Rng>
+__device__ __forceinline__ void dq_push(const G& g, Rng& rng, uint32_t* q, int64_t stride)
+{
+    uint32_t hdr = q[0];
+    const uint32_t cnt = hdr & 7u, head = (hdr >> 3) & 3u, p0 = rng.pos;
+    uint32_t e0, e1;
+    g.make_deal(rng, hdr, e0, e1);
+    uint32_t d = rng.pos >= p0 ? rng.pos - p0 : rng.pos + (uint32_t)RING - p0;
+    d = d < 511u ? d : 511u;
+    const uint32_t slot = (head + cnt) & (uint32_t)(G::DQ - 1);
+    q[(1 + 2 * slot) * stride] = e0 | (d & 127u) << 25;
+    q[(2 + 2 * slot) * stride] = e1 | (d >> 7) << 30;
+    q[0] = (hdr & ~7u) | (cnt + 1u);
+}
+
+// Game.init_game: the oldest queued deal, or a deal drawn now when the queue is empty
+template <class G, class Rng>
+__device__ __forceinline__ void dq_reset(G& g, Rng& rng, uint32_t* q, int64_t stride)
+{
+    uint32_t hdr = q[0], e0, e1;
+    const uint32_t cnt = hdr & 7u, head = (hdr >> 3) & 3u;
+    if (cnt) {
+        e0 = q[(1 + 2 * head) * stride];
+        e1 = q[(2 + 2 * head) * stride];
+        hdr = (hdr & ~0x1Fu) | (cnt - 1u) | ((head + 1u) & (uint32_t)(G::DQ - 1)) << 3;
+    } else {
+        g.make_deal(rng, hdr, e0, e1);
+    }
+    q[0] = hdr;
+    g.reset_from(e0, e1);
+}
+
+// reset of the env's game through its deal queue where the game has one
+template <class G, class Rng>
+__device__ __forceinline__ void game_reset(G& g, Rng& rng, uint32_t* st, int64_t n, int64_t env)
+{
+    if constexpr (DqOf<G>::value > 0) dq_reset(g, rng, st + (int64_t)G::GW * n + env, n);
+    else g.reset(rng);
+}
+
 #define CS_SMEM_ROWS(G, ROWS)                                         \
     __shared__ uint32_t lds[WAVES_PER_BLOCK][ObsLds<G, ROWS>::WORDS]; \
     __shared__ uint32_t scr[WAVES_PER_BLOCK][Scratch<G>::WORDS]
@@ -215,6 +268,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed(uint32_t* mt, uint32_t* ctl, uin
         g.bind(scratch_of<G>(scr[threadIdx.x / WAVE], lane), prm);
         g.blank();
         g.store(st, n, env);
+        if constexpr (DqOf<G>::value > 0) st[(int64_t)G::GW * n + env] = 0u;   // empty deal queue
         ctl[env] = 0u | (uint32_t)(RING_GEN - 1) << 12;          // position 0, latest block in slot 2
         return;
     }
@@ -253,7 +307,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, ui
     g.blank();
     if (c.valid) {
         g.load(st, n, c.env);   // the Game object outlives init_game (limit-holdem's raise history, :98/:101)
-        g.reset(m);
+        game_reset(g, m, st, n, c.env);
     }
     refill<G>(m, c.lane, flags & 1);
     uint32_t bits[G::NB];
@@ -293,7 +347,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uin
     if (c.valid) {
         g.load(st, n, c.env);
         if (g.is_over()) {
-            g.reset(m);
+            game_reset(g, m, st, n, c.env);
         } else {
             g.step(actions[c.env], m);
             done = g.is_over();
@@ -362,12 +416,26 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
             stage_rows_copy<G::STAGE_W, G::STAGE_PAD>(stage[c.wid], rows, c.lane, c.nvalid, true);
         }
     }
+    // the deal queues of the wave's envs in LDS for the launch (DQW consecutive words per lane: odd stride)
+    constexpr int DQ = DqOf<G>::value, DQW = DqOf<G>::words;
+    __shared__ uint32_t dql[DQ > 0 ? WAVES_PER_BLOCK * G::EPW * DQW : 1];
+    uint32_t* q = dql;
+    if constexpr (DQ > 0) {
+        q = dql + (c.wid * G::EPW + (c.lane < G::EPW ? c.lane : 0)) * DQW;
+        if (c.valid) {
+#pragma unroll
+            for (int w = 0; w < DQW; w++) q[w] = st[(int64_t)(G::GW + w) * n + c.env];
+        }
+    }
     G g;
     g.bind(scratch_of<G>(scr[c.wid], c.lane), prm);
     g.blank();
     if (c.valid) {
         g.load(st, n, c.env);
-        if (g.is_over()) g.reset(m);
+        if (g.is_over()) {
+            if constexpr (DQ > 0) dq_reset(g, m, q, 1);
+            else g.reset(m);
+        }
     }
     refill<G>(m, c.lane, flags & 1);
     if (staged) restage<G>(m, stage[c.wid], c.lane, c.valid);
@@ -419,7 +487,16 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
             emit_reward<G>(reward, row, r);
             done_o[row] = (uint8_t)done;
 #endif
-            if (done) g.reset(m);
+            if constexpr (DQ == 0) {
+                if (done) g.reset(m);
+            }
+        }
+        if constexpr (DQ > 0) {
+            // a lane ending its game with an empty queue makes every lane with room draw one deal ahead, in lockstep
+            if (__ballot(c.valid && done && (q[0] & 7u) == 0u)) {
+                if (c.valid && (q[0] & 7u) < (uint32_t)DQ) dq_push(g, m, q, 1);
+            }
+            if (c.valid && done) dq_reset(g, m, q, 1);
         }
         refill<G>(m, c.lane, flags & 1);
         if (staged) restage<G>(m, stage[c.wid], c.lane, c.valid);
@@ -433,6 +510,10 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
     }
     if (c.valid) {
         g.store(st, n, c.env);
+        if constexpr (DQ > 0) {
+#pragma unroll
+            for (int w = 0; w < DQW; w++) st[(int64_t)(G::GW + w) * n + c.env] = q[w];
+        }
         ctl[c.env] = m.ctl_word() | ((uint32_t)keep << 17);
         if (keep) sctl[c.env] = m.sp | (m.sn << 16);
     }

@@ -204,8 +204,24 @@ __device__ __forceinline__ void holdem_deal2(Rng& rng, uint32_t& holes, uint32_t
     board = d1;
 }
 
+// Deal queue (hold'em games): a hold'em deal depends only on the env's MT stream, never on the actions, so the
+// rollout draws deals ahead -- one pass of all lanes with room in their queue, in lockstep, whenever a lane ends a
+// game with its queue empty -- instead of a pass at every step in which any lane of the wave resets (a 32-env wave
+// has a reset almost every step, with ~2/5 of its lanes active). Same deals in the same stream order, so outputs are
+// unchanged. The queue lives after the game's words in the env state: a header (count:3, head:2, no-limit dealer
+// drawn << 5, dealer << 6) and DQ entries of two words (e0 = holes | seat bit << 24 | draws[6:0] << 25, e1 = board |
+// draws[8:7] << 30; draws = MT words the deal consumed, for the host's stream position, saturating at 511).
+#ifndef CS_DEAL_QUEUE
+#define CS_DEAL_QUEUE 4
+#endif
+constexpr int HOLDEM_DQ = CS_DEAL_QUEUE;
+static_assert(HOLDEM_DQ == 0 || HOLDEM_DQ == 2 || HOLDEM_DQ == 4, "deal queue: 2-bit head, power-of-two ring");
+constexpr int HOLDEM_DQ_WORDS = HOLDEM_DQ > 0 ? 1 + 2 * HOLDEM_DQ : 0;
+
 struct Limit {
-    static constexpr int OBS = 72, A = 4, P = 2, LB = 1, WORDS = 4, ACTION_BYTES = 1;
+    static constexpr int GW = 4;                        // game words; the deal queue follows
+    static constexpr int DQ = HOLDEM_DQ;
+    static constexpr int OBS = 72, A = 4, P = 2, LB = 1, WORDS = GW + HOLDEM_DQ_WORDS, ACTION_BYTES = 1;
     static constexpr int NB = 3;
     static constexpr bool RING = true;          // MT stream as the byte ring (cs_ring.h)
     static constexpr bool RAW_OBS = false;
@@ -273,12 +289,26 @@ struct Limit {
         for (int i = 0; i < 4; i++) set_bit(bits, 52 + 5 * i + (int)((rn >> (3 * i)) & 7u));
     }
 
+    // the deal of init_game (game.py:46-95): shuffle + holes + board, then the small blind seat randint(0, 2)
     template <class Rng>
-    __device__ __forceinline__ void reset(Rng& rng)
+    __device__ __forceinline__ void make_deal(Rng& rng, uint32_t&, uint32_t& e0, uint32_t& e1) const
     {
         uint32_t d0, d1;
         holdem_deal2(rng, d0, d1);
-        const int s = (int)rng.interval(1u);
+        e0 = d0 | rng.interval(1u) << 24;
+        e1 = d1;
+    }
+    template <class Rng>
+    __device__ __forceinline__ void reset(Rng& rng)
+    {
+        uint32_t hdr = 0, e0, e1;
+        make_deal(rng, hdr, e0, e1);
+        reset_from(e0, e1);
+    }
+    __device__ __forceinline__ void reset_from(uint32_t e0, uint32_t e1)
+    {
+        const uint32_t d0 = e0 & 0xFFFFFFu, d1 = e1 & 0x3FFFFFFFu;
+        const int s = (int)((e0 >> 24) & 1u);
         const int in_0 = s == 0 ? 1 : 2, in_1 = s == 0 ? 2 : 1;
         const int first = s;  // (BB + 1) % 2 with BB = (s + 1) % 2
         w0 = d0 | (uint32_t)in_0 << 24 | (uint32_t)first << 30;

@@ -35,7 +35,9 @@
 namespace cs {
 
 struct Nolimit {
-    static constexpr int OBS = 54, A = 5, P = 2, LB = 1, WORDS = 4, ACTION_BYTES = 1;
+    static constexpr int GW = 4;                        // game words; the deal queue follows (cs_limit.h)
+    static constexpr int DQ = HOLDEM_DQ;
+    static constexpr int OBS = 54, A = 5, P = 2, LB = 1, WORDS = GW + HOLDEM_DQ_WORDS, ACTION_BYTES = 1;
     static constexpr int NB = 14;               // raw obs bytes, four per word (RowWriterRaw)
     static constexpr bool RING = true;          // MT stream as the byte ring (cs_ring.h)
     static constexpr bool RAW_OBS = true;
@@ -109,15 +111,30 @@ struct Nolimit {
         raw[13] = (uint32_t)(player ? b : a) | (uint32_t)(a > b ? a : b) << 8;
     }
 
+    // the dealer seat randint(0, 2) before the first game's shuffle (game.py:62-63; kept by later games of the env,
+    // hdr bits 5 / 6 of the deal queue header), then the hold'em deal
+    template <class Rng>
+    __device__ __forceinline__ void make_deal(Rng& rng, uint32_t& hdr, uint32_t& e0, uint32_t& e1) const
+    {
+        uint32_t dealer;
+        if (dealer_cfg >= 0) dealer = (uint32_t)dealer_cfg;
+        else if ((hdr >> 5) & 1u) dealer = (hdr >> 6) & 1u;
+        else dealer = rng.interval(1u);
+        hdr = (hdr & ~0x60u) | 1u << 5 | dealer << 6;
+        holdem_deal2(rng, e0, e1);
+        e0 |= dealer << 24;
+    }
     template <class Rng>
     __device__ __forceinline__ void reset(Rng& rng)
     {
-        int dealer;
-        if (dealer_cfg >= 0) dealer = dealer_cfg;
-        else if ((w0 >> 26) & 1) dealer = (w0 >> 25) & 1;     // drawn by an earlier game of this env
-        else dealer = (int)rng.interval(1u);                  // randint(0, 2), before the deal
-        uint32_t holes, brd;
-        holdem_deal2(rng, holes, brd);
+        uint32_t hdr = ((w0 >> 26) & 1u) << 5 | ((w0 >> 25) & 1u) << 6, e0, e1;   // drawn by an earlier game
+        make_deal(rng, hdr, e0, e1);
+        reset_from(e0, e1);
+    }
+    __device__ __forceinline__ void reset_from(uint32_t e0, uint32_t e1)
+    {
+        const uint32_t holes = e0 & 0xFFFFFFu, brd = e1 & 0x3FFFFFFFu;
+        const int dealer = (int)((e0 >> 24) & 1u);
         const int s = dealer ^ 1, b = dealer;            // SB (dealer + 1), BB (dealer + 2) = dealer
         const int bb = chips < 2 ? chips : 2, sb = chips < 1 ? chips : 1;
         const int i0 = b == 0 ? bb : sb, i1 = b == 0 ? sb : bb;

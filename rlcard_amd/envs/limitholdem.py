@@ -27,7 +27,7 @@ class LimitholdemEnv(Env):
         return self.actions[action_id]
 
     def _fields(self):
-        w0, w1, w2, w3 = self._state_words()
+        w0, w1, w2, w3 = self._state_words()[:4]
         rc = (w2 >> 21) & 7
         nboard = 0 if rc == 0 else min(5, rc + 2)
         return dict(hands=[[w0 & 63, (w0 >> 6) & 63], [(w0 >> 12) & 63, (w0 >> 18) & 63]],

@@ -49,7 +49,7 @@ class NolimitholdemEnv(Env):
         return raw.value if isinstance(raw, Action) else int(raw)
 
     def _fields(self):
-        w0, w1, w2, w3 = self._state_words()
+        w0, w1, w2, w3 = self._state_words()[:4]
         rc = (w0 >> 27) & 7
         nboard = 0 if rc == 0 else min(5, rc + 2)
         chips = [w2 & 255, (w2 >> 8) & 255]

@@ -151,6 +151,30 @@ def test_rollout_matches_oracle(oracle, game, name, flags):
         assert v.rng_position(i) == ob.draws(i) % v.rng_period
 
 
+@pytest.mark.parametrize('game', ['limit-holdem', 'no-limit-holdem', 'leduc-holdem'])
+def test_rollout_step_reset_interleaved(oracle, game):
+    """Rollout launches, single steps and resets on the same envs: the hold'em deal queue (deals the rollout drew
+    ahead) is consumed by cs_step / cs_reset in stream order, and the host's stream position discounts it."""
+    n, T = 1000 + 13, 24
+    seeds = list(range(300, 300 + n))
+    v = _vec(game, n, seed=300)
+    ob = _oracle_batch(oracle, game, seeds)
+    rng = np.random.RandomState(3)
+    _assert_same(_np(v.reset()), ob.reset(), 'reset')
+    t0 = 0
+    for rnd in range(3):
+        _assert_same(_np(v.rollout(T, policy_seed=11, t0=t0)), ob.rollout(T, 11, t0, 0), 'rollout %d' % rnd)
+        t0 += T
+        for t in range(5):
+            acts = rng.randint(0, v.num_actions, size=n).astype(np.int32)
+            _assert_same(_np(v.step(torch.from_numpy(acts).cuda())), ob.step(acts), 'step %d.%d' % (rnd, t))
+        torch.cuda.synchronize()
+        for i in (0, 1, n // 2, n - 1):
+            assert v.rng_position(i) == ob.draws(i) % v.rng_period
+        if rnd == 1:
+            _assert_same(_np(v.reset()), ob.reset(), 'reset %d' % rnd)
+
+
 @pytest.mark.parametrize('game,name', GAMES)
 def test_full_size_rollout_properties_and_sampled_parity(oracle, game, name):
     n, T, win = FULL_SIZE[game]
