@@ -208,10 +208,10 @@ __device__ __forceinline__ void dq_push(const G& g, Rng& rng, uint32_t* q, int64
     g.make_deal(rng, hdr, e0, e1);
     uint32_t d = rng.pos >= p0 ? rng.pos - p0 : rng.pos + (uint32_t)RING - p0;
     d = d < 511u ? d : 511u;
-    const uint32_t slot = (head + cnt) & (uint32_t)(G::DQ - 1);
+    const uint32_t slot = (head + cnt) & (uint32_t)(G::DQ - 1), hi = 7u + 2u * slot;
     q[(1 + 2 * slot) * stride] = e0 | (d & 127u) << 25;
-    q[(2 + 2 * slot) * stride] = e1 | (d >> 7) << 30;
-    q[0] = (hdr & ~7u) | (cnt + 1u);
+    q[(2 + 2 * slot) * stride] = e1;
+    q[0] = (hdr & ~7u & ~(3u << hi)) | (d >> 7) << hi | (cnt + 1u);
 }
 
 // Game.init_game: the oldest queued deal, or a deal drawn now when the queue is empty

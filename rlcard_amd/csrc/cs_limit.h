@@ -204,13 +204,31 @@ __device__ __forceinline__ void holdem_deal2(Rng& rng, uint32_t& holes, uint32_t
     board = d1;
 }
 
+// the showdown of a heads-up deal when both players stay in (Judger.judge_game -> compare_hands, judger.py:11-108,
+// utils.py): bit 0 = player 0 wins or ties, bit 1 = player 1. It depends on the deal alone: no-limit evaluates it when
+// the deal is drawn (in the rollout's lockstep deal passes) and keeps it in the state; limit at the game's end.
+__device__ __forceinline__ uint32_t holdem_showdown(uint32_t holes, uint32_t board)
+{
+    uint64_t bc = 0, bs = 0;
+#pragma unroll
+    for (int k = 0; k < 5; k++) tally_card((int)((board >> (6 * k)) & 63u), bc, bs);
+    uint64_t c0 = bc, s0 = bs, c1 = bc, s1 = bs;
+    tally_card((int)(holes & 63u), c0, s0);
+    tally_card((int)((holes >> 6) & 63u), c0, s0);
+    tally_card((int)((holes >> 12) & 63u), c1, s1);
+    tally_card((int)((holes >> 18) & 63u), c1, s1);
+    const uint32_t v0 = holdem_rank7(c0, s0), v1 = holdem_rank7(c1, s1);
+    return (uint32_t)(v0 >= v1) | (uint32_t)(v1 >= v0) << 1;
+}
+
 // Deal queue (hold'em games): a hold'em deal depends only on the env's MT stream, never on the actions, so the
 // rollout draws deals ahead -- one pass of all lanes with room in their queue, in lockstep, whenever a lane ends a
 // game with its queue empty -- instead of a pass at every step in which any lane of the wave resets (a 32-env wave
 // has a reset almost every step, with ~2/5 of its lanes active). Same deals in the same stream order, so outputs are
 // unchanged. The queue lives after the game's words in the env state: a header (count:3, head:2, no-limit dealer
-// drawn << 5, dealer << 6) and DQ entries of two words (e0 = holes | seat bit << 24 | draws[6:0] << 25, e1 = board |
-// draws[8:7] << 30; draws = MT words the deal consumed, for the host's stream position, saturating at 511).
+// drawn << 5, dealer << 6, draws[8:7] of slot k << 7 + 2 k) and DQ entries of two words (e0 = holes | seat bit << 24 |
+// draws[6:0] << 25, e1 = board | showdown << 30; draws = MT words the deal consumed, for the host's stream position,
+// saturating at 511).
 #ifndef CS_DEAL_QUEUE
 #define CS_DEAL_QUEUE 4
 #endif
@@ -296,7 +314,7 @@ struct Limit {
         uint32_t d0, d1;
         holdem_deal2(rng, d0, d1);
         e0 = d0 | rng.interval(1u) << 24;
-        e1 = d1;
+        e1 = d1;   // showdown at the game's end: evaluated with the deal it measured slower here (no-limit: faster)
     }
     template <class Rng>
     __device__ __forceinline__ void reset(Rng& rng)
@@ -307,7 +325,7 @@ struct Limit {
     }
     __device__ __forceinline__ void reset_from(uint32_t e0, uint32_t e1)
     {
-        const uint32_t d0 = e0 & 0xFFFFFFu, d1 = e1 & 0x3FFFFFFFu;
+        const uint32_t d0 = e0 & 0xFFFFFFu, d1 = e1;
         const int s = (int)((e0 >> 24) & 1u);
         const int in_0 = s == 0 ? 1 : 2, in_1 = s == 0 ? 2 : 1;
         const int first = s;  // (BB + 1) % 2 with BB = (s + 1) % 2
@@ -350,22 +368,9 @@ struct Limit {
         if (f0() || f1()) {
             win0 = !f0(); win1 = !f1();
         } else {
-            uint64_t bc = 0, bs = 0;
-#pragma unroll
-            for (int k = 0; k < 5; k++) tally_card(board(k), bc, bs);
-            uint64_t c0 = bc, s0 = bs;
-            tally_card(hole(0, 0), c0, s0);
-            tally_card(hole(0, 1), c0, s0);
-#ifdef CS_PROF_NO_EVAL   // profiling builds only: wrong payoffs, timing of the evaluator
-            const uint32_t v0 = (uint32_t)(c0 ^ s0), v1 = (uint32_t)(bc ^ bs);
-#else
-            const uint32_t v0 = holdem_rank7(c0, s0);
-            uint64_t c1 = bc, s1 = bs;
-            tally_card(hole(1, 0), c1, s1);
-            tally_card(hole(1, 1), c1, s1);
-            const uint32_t v1 = holdem_rank7(c1, s1);
-#endif
-            win0 = v0 >= v1; win1 = v1 >= v0;
+            const uint32_t sd = holdem_showdown(w0 & 0xFFFFFFu, w1);
+            win0 = (int)(sd & 1u);
+            win1 = (int)(sd >> 1);
         }
         const int a = in0(), b = in1(), m = a < b ? a : b;
         float p0 = 0.f, p1 = 0.f;

@@ -21,7 +21,7 @@
 // Packed state, 4 u32 words per env (word-major [4][N]):
 //   w0: holes p0c0 p0c1 p1c0 p1c1 6 bits each (0..23), ptr (24), dealer (25), dealer drawn (26), rc:3 (27..29),
 //       over (31)
-//   w1: board c0..c4 6 bits each (0..29)
+//   w1: board c0..c4 6 bits each (0..29), showdown win0 / win1 (30, 31; holdem_showdown)
 //   w2: in0:8 in1:8 raised0:8 raised1:8
 //   w3: status0:2 status1:2 (0 alive, 1 folded, 2 all-in), not_raise_num:4 (4..7), not_playing_num:4 (8..11)
 #pragma once
@@ -122,6 +122,7 @@ struct Nolimit {
         else dealer = rng.interval(1u);
         hdr = (hdr & ~0x60u) | 1u << 5 | dealer << 6;
         holdem_deal2(rng, e0, e1);
+        e1 |= holdem_showdown(e0, e1) << 30;
         e0 |= dealer << 24;
     }
     template <class Rng>
@@ -133,7 +134,7 @@ struct Nolimit {
     }
     __device__ __forceinline__ void reset_from(uint32_t e0, uint32_t e1)
     {
-        const uint32_t holes = e0 & 0xFFFFFFu, brd = e1 & 0x3FFFFFFFu;
+        const uint32_t holes = e0 & 0xFFFFFFu, brd = e1;   // board + showdown
         const int dealer = (int)((e0 >> 24) & 1u);
         const int s = dealer ^ 1, b = dealer;            // SB (dealer + 1), BB (dealer + 2) = dealer
         const int bb = chips < 2 ? chips : 2, sb = chips < 1 ? chips : 1;
@@ -195,19 +196,9 @@ struct Nolimit {
         int win0, win1;
         if (s0 == FOLDED || s1 == FOLDED) {
             win0 = s0 != FOLDED; win1 = s1 != FOLDED;
-        } else {
-            uint64_t bc = 0, bs = 0;
-#pragma unroll
-            for (int k = 0; k < 5; k++) tally_card(board(k), bc, bs);
-            uint64_t c0 = bc, q0 = bs;
-            tally_card(hole(0, 0), c0, q0);
-            tally_card(hole(0, 1), c0, q0);
-            const uint32_t v0 = holdem_rank7(c0, q0);
-            uint64_t c1 = bc, q1 = bs;
-            tally_card(hole(1, 0), c1, q1);
-            tally_card(hole(1, 1), c1, q1);
-            const uint32_t v1 = holdem_rank7(c1, q1);
-            win0 = v0 >= v1; win1 = v1 >= v0;
+        } else {   // showdown, evaluated with the deal (holdem_showdown)
+            win0 = (int)((w1 >> 30) & 1u);
+            win1 = (int)(w1 >> 31);
         }
         const int a = in(0), b = in(1), m = a < b ? a : b;
         float p0 = 0.f;

@@ -232,8 +232,7 @@ class VecEnv:
             hdr = w[gw]
             for k in range(hdr & 7):
                 slot = (((hdr >> 3) & 3) + k) % cap
-                e0, e1 = w[gw + 1 + 2 * slot], w[gw + 2 + 2 * slot]
-                pos -= ((e0 >> 25) & 127) | ((e1 >> 30) & 3) << 7
+                pos -= ((w[gw + 1 + 2 * slot] >> 25) & 127) | ((hdr >> (7 + 2 * slot)) & 3) << 7
         return pos % self.rng_period
 
     def set_kernel_flags(self, flags):
