@@ -162,7 +162,10 @@ int cs_cfr_train(cs_handle* h, int32_t iterations, int64_t iteration0, double* p
                  double* regrets, uint32_t* flags, void* stream);
 
 /* Copy the packed state words of env `env` (state_words u32, HOST buffer) -- the raw fields behind
- * Env.get_state()['raw_obs'] / get_perfect_information for single-env compatibility and debugging. Synchronous. */
+ * Env.get_state()['raw_obs'] / get_perfect_information for single-env compatibility and debugging. Limit and
+ * No-limit hold'em: 4 game words, then the env's deal queue (deals the rollout drew ahead from the stream; a header
+ * word -- count in bits 0..2, head in 3..4 -- and 4 entries of two words, e0 bits 25..31 + header bits 7 + 2 slot ..
+ * 8 + 2 slot = MT draws of the entry). Synchronous. */
 int cs_get_env_state(cs_handle* h, int64_t env, uint32_t* host_words, int32_t nwords);
 
 /* Overwrite the packed state words of env `env` from a HOST buffer taken by cs_get_env_state: Env.step_back
@@ -170,7 +173,8 @@ int cs_get_env_state(cs_handle* h, int64_t env, uint32_t* host_words, int32_t nw
  * reference's np_random is not part of the restored history. Synchronous. */
 int cs_set_env_state(cs_handle* h, int64_t env, const uint32_t* host_words, int32_t nwords);
 
-/* Stream position (u32 draws consumed) bookkeeping word of env `env` (HOST out). Synchronous; for parity tests. */
+/* Stream position (u32 draws consumed) bookkeeping word of env `env` (HOST out). Synchronous; for parity tests.
+ * Hold'em envs: the position includes the draws of the queued deals (see cs_get_env_state). */
 int cs_get_rng_ctl(cs_handle* h, int64_t env, uint32_t* host_ctl);
 
 /* Testing hook: when enabled, the wave-cooperative MT refill is skipped, so every block crossing takes the in-lane
