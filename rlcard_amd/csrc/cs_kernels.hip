@@ -192,42 +192,69 @@ __device__ __forceinline__ uint32_t* scratch_of(uint32_t* wave_area, int lane)
 template <class G, class = void>
 struct DqOf {
     static constexpr int value = 0, words = 0;
+    static constexpr bool regs = false;
 };
 template <class G>
 struct DqOf<G, std::void_t<decltype(G::DQ)>> {
     static constexpr int value = G::DQ, words = G::DQ > 0 ? 1 + 2 * G::DQ : 0;
+    static constexpr bool regs = G::DQ_REGS;
+};
+
+// queue word views: DqMem = words `stride` apart (state in HBM: n; LDS copy: 1), DqRegs = the words in registers
+// (dynamic slots through select chains, so the array never goes to scratch)
+struct DqMem {
+    uint32_t* p;
+    int64_t stride;
+    __device__ __forceinline__ uint32_t get(uint32_t i) const { return p[i * stride]; }
+    __device__ __forceinline__ void set(uint32_t i, uint32_t v) { p[i * stride] = v; }
+};
+template <int NW>
+struct DqRegs {
+    uint32_t w[NW];
+    __device__ __forceinline__ uint32_t get(uint32_t i) const
+    {
+        uint32_t r = w[0];
+#pragma unroll
+        for (int k = 1; k < NW; k++) r = i == (uint32_t)k ? w[k] : r;
+        return r;
+    }
+    __device__ __forceinline__ void set(uint32_t i, uint32_t v)
+    {
+#pragma unroll
+        for (int k = 0; k < NW; k++) w[k] = i == (uint32_t)k ? v : w[k];
+    }
 };
 
 // draw the env's next deal into its queue (the caller checks for room)
-template <class G, class Rng>
-__device__ __forceinline__ void dq_push(const G& g, Rng& rng, uint32_t* q, int64_t stride)
+template <class G, class Rng, class Q>
+__device__ __forceinline__ void dq_push(const G& g, Rng& rng, Q& q)
 {
-    uint32_t hdr = q[0];
+    uint32_t hdr = q.get(0);
     const uint32_t cnt = hdr & 7u, head = (hdr >> 3) & 3u, p0 = rng.pos;
     uint32_t e0, e1;
     g.make_deal(rng, hdr, e0, e1);
     uint32_t d = rng.pos >= p0 ? rng.pos - p0 : rng.pos + (uint32_t)RING - p0;
     d = d < 511u ? d : 511u;
     const uint32_t slot = (head + cnt) & (uint32_t)(G::DQ - 1), hi = 7u + 2u * slot;
-    q[(1 + 2 * slot) * stride] = e0 | (d & 127u) << 25;
-    q[(2 + 2 * slot) * stride] = e1;
-    q[0] = (hdr & ~7u & ~(3u << hi)) | (d >> 7) << hi | (cnt + 1u);
+    q.set(1 + 2 * slot, e0 | (d & 127u) << 25);
+    q.set(2 + 2 * slot, e1);
+    q.set(0, (hdr & ~7u & ~(3u << hi)) | (d >> 7) << hi | (cnt + 1u));
 }
 
 // Game.init_game: the oldest queued deal, or a deal drawn now when the queue is empty
-template <class G, class Rng>
-__device__ __forceinline__ void dq_reset(G& g, Rng& rng, uint32_t* q, int64_t stride)
+template <class G, class Rng, class Q>
+__device__ __forceinline__ void dq_reset(G& g, Rng& rng, Q& q)
 {
-    uint32_t hdr = q[0], e0, e1;
+    uint32_t hdr = q.get(0), e0, e1;
     const uint32_t cnt = hdr & 7u, head = (hdr >> 3) & 3u;
     if (cnt) {
-        e0 = q[(1 + 2 * head) * stride];
-        e1 = q[(2 + 2 * head) * stride];
+        e0 = q.get(1 + 2 * head);
+        e1 = q.get(2 + 2 * head);
         hdr = (hdr & ~0x1Fu) | (cnt - 1u) | ((head + 1u) & (uint32_t)(G::DQ - 1)) << 3;
     } else {
         g.make_deal(rng, hdr, e0, e1);
     }
-    q[0] = hdr;
+    q.set(0, hdr);
     g.reset_from(e0, e1);
 }
 
@@ -235,8 +262,12 @@ __device__ __forceinline__ void dq_reset(G& g, Rng& rng, uint32_t* q, int64_t st
 template <class G, class Rng>
 __device__ __forceinline__ void game_reset(G& g, Rng& rng, uint32_t* st, int64_t n, int64_t env)
 {
-    if constexpr (DqOf<G>::value > 0) dq_reset(g, rng, st + (int64_t)G::GW * n + env, n);
-    else g.reset(rng);
+    if constexpr (DqOf<G>::value > 0) {
+        DqMem q{st + (int64_t)G::GW * n + env, n};
+        dq_reset(g, rng, q);
+    } else {
+        g.reset(rng);
+    }
 }
 
 #define CS_SMEM_ROWS(G, ROWS)                                         \
@@ -416,15 +447,18 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
             stage_rows_copy<G::STAGE_W, G::STAGE_PAD>(stage[c.wid], rows, c.lane, c.nvalid, true);
         }
     }
-    // the deal queues of the wave's envs in LDS for the launch (DQW consecutive words per lane: odd stride)
+    // the deal queues of the wave's envs for the launch: in registers, or in LDS (DQW consecutive words per lane:
+    // odd stride), per the game's DQ_REGS
     constexpr int DQ = DqOf<G>::value, DQW = DqOf<G>::words;
-    __shared__ uint32_t dql[DQ > 0 ? WAVES_PER_BLOCK * G::EPW * DQW : 1];
-    uint32_t* q = dql;
+    constexpr bool QREGS = DqOf<G>::regs;
+    __shared__ uint32_t dql[DQ > 0 && !QREGS ? WAVES_PER_BLOCK * G::EPW * DQW : 1];
+    using QV = std::conditional_t<QREGS, DqRegs<DQW ? DQW : 1>, DqMem>;
+    QV q{};
     if constexpr (DQ > 0) {
-        q = dql + (c.wid * G::EPW + (c.lane < G::EPW ? c.lane : 0)) * DQW;
+        if constexpr (!QREGS) q = DqMem{dql + (c.wid * G::EPW + (c.lane < G::EPW ? c.lane : 0)) * DQW, 1};
         if (c.valid) {
 #pragma unroll
-            for (int w = 0; w < DQW; w++) q[w] = st[(int64_t)(G::GW + w) * n + c.env];
+            for (int w = 0; w < DQW; w++) q.set(w, st[(int64_t)(G::GW + w) * n + c.env]);
         }
     }
     G g;
@@ -433,7 +467,7 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
     if (c.valid) {
         g.load(st, n, c.env);
         if (g.is_over()) {
-            if constexpr (DQ > 0) dq_reset(g, m, q, 1);
+            if constexpr (DQ > 0) dq_reset(g, m, q);
             else g.reset(m);
         }
     }
@@ -493,10 +527,10 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
         }
         if constexpr (DQ > 0) {
             // a lane ending its game with an empty queue makes every lane with room draw one deal ahead, in lockstep
-            if (__ballot(c.valid && done && (q[0] & 7u) == 0u)) {
-                if (c.valid && (q[0] & 7u) < (uint32_t)DQ) dq_push(g, m, q, 1);
+            if (__ballot(c.valid && done && (q.get(0) & 7u) == 0u)) {
+                if (c.valid && (q.get(0) & 7u) < (uint32_t)DQ) dq_push(g, m, q);
             }
-            if (c.valid && done) dq_reset(g, m, q, 1);
+            if (c.valid && done) dq_reset(g, m, q);
         }
         refill<G>(m, c.lane, flags & 1);
         if (staged) restage<G>(m, stage[c.wid], c.lane, c.valid);
@@ -512,7 +546,7 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
         g.store(st, n, c.env);
         if constexpr (DQ > 0) {
 #pragma unroll
-            for (int w = 0; w < DQW; w++) st[(int64_t)(G::GW + w) * n + c.env] = q[w];
+            for (int w = 0; w < DQW; w++) st[(int64_t)(G::GW + w) * n + c.env] = q.get(w);
         }
         ctl[c.env] = m.ctl_word() | ((uint32_t)keep << 17);
         if (keep) sctl[c.env] = m.sp | (m.sn << 16);

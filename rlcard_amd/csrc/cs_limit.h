@@ -37,6 +37,9 @@
 #ifndef CS_LIMIT_MIN_WAVES
 #define CS_LIMIT_MIN_WAVES 5
 #endif
+#ifndef CS_LIMIT_DQ_REGS
+#define CS_LIMIT_DQ_REGS 0
+#endif
 #ifndef CS_LIMIT_EPW
 #define CS_LIMIT_EPW 32
 #endif
@@ -239,6 +242,7 @@ constexpr int HOLDEM_DQ_WORDS = HOLDEM_DQ > 0 ? 1 + 2 * HOLDEM_DQ : 0;
 struct Limit {
     static constexpr int GW = 4;                        // game words; the deal queue follows
     static constexpr int DQ = HOLDEM_DQ;
+    static constexpr bool DQ_REGS = CS_LIMIT_DQ_REGS;          // rollout: queue in registers, else LDS
     static constexpr int OBS = 72, A = 4, P = 2, LB = 1, WORDS = GW + HOLDEM_DQ_WORDS, ACTION_BYTES = 1;
     static constexpr int NB = 3;
     static constexpr bool RING = true;          // MT stream as the byte ring (cs_ring.h)

@@ -28,6 +28,12 @@
 #include "cs_device.h"
 #include "cs_limit.h"
 
+#ifndef CS_NOLIMIT_DQ_REGS
+#define CS_NOLIMIT_DQ_REGS 0
+#endif
+#ifndef CS_NOLIMIT_EPW
+#define CS_NOLIMIT_EPW 32
+#endif
 #ifndef CS_NOLIMIT_MIN_WAVES
 #define CS_NOLIMIT_MIN_WAVES 5
 #endif
@@ -37,6 +43,7 @@ namespace cs {
 struct Nolimit {
     static constexpr int GW = 4;                        // game words; the deal queue follows (cs_limit.h)
     static constexpr int DQ = HOLDEM_DQ;
+    static constexpr bool DQ_REGS = CS_NOLIMIT_DQ_REGS;          // rollout: queue in registers, else LDS
     static constexpr int OBS = 54, A = 5, P = 2, LB = 1, WORDS = GW + HOLDEM_DQ_WORDS, ACTION_BYTES = 1;
     static constexpr int NB = 14;               // raw obs bytes, four per word (RowWriterRaw)
     static constexpr bool RING = true;          // MT stream as the byte ring (cs_ring.h)
@@ -46,7 +53,7 @@ struct Nolimit {
     static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_PAD = 8, STAGE_R = 100;
     static constexpr int RESTAGE_B = 8;
     static constexpr int MIN_WAVES = CS_NOLIMIT_MIN_WAVES;
-    static constexpr int EPW = 32;
+    static constexpr int EPW = CS_NOLIMIT_EPW;
     static constexpr int REFILL_K = 2;
     enum { FOLD = 0, CHECK_CALL = 1, RAISE_HALF_POT = 2, RAISE_POT = 3, ALL_IN = 4 };
     enum { ALIVE = 0, FOLDED = 1, ALLIN = 2 };
