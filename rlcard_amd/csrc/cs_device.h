@@ -17,6 +17,29 @@
 
 namespace cs {
 
+// rollout output stores: nontemporal (streamed past the caches: written once, GBs per launch, read by the consumer
+// long after), measured faster than default-policy stores (Leduc 2.37 -> 2.08 ms, Limit 1.39 -> 1.33 ms per launch);
+// CS_OUT_NT=0 for A/B runs
+#ifndef CS_OUT_NT
+#define CS_OUT_NT 1
+#endif
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void out_store16(uint4* p, const uint4& v)
+{
+    if constexpr (CS_OUT_NT) {
+        const u32x4_t x = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(x, (u32x4_t*)p);
+    } else {
+        *p = v;
+    }
+}
+template <class T>
+__device__ __forceinline__ void out_store(T* p, T v)
+{
+    if constexpr (CS_OUT_NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 constexpr int MT_N = 624;
 constexpr int MT_M = 397;
 constexpr int MT_WORDS = 2 * MT_N;
@@ -520,7 +543,7 @@ struct RowWriter {
 #pragma unroll
             for (int j = 0; j < (Q + WAVE - 1) / WAVE; j++) {
                 const int q = j * WAVE + lane;
-                if (q < Q) o[q] = src[q];
+                if (q < Q) out_store16(o + q, src[q]);
             }
         } else {
             uint32_t* o = (uint32_t*)out_span;
@@ -568,7 +591,7 @@ struct RowWriterRaw {
 #pragma unroll
             for (int j = 0; j < (SPAN / 16 + WAVE - 1) / WAVE; j++) {
                 const int q = j * WAVE + lane;
-                if (q < SPAN / 16) o[q] = src[q];
+                if (q < SPAN / 16) out_store16(o + q, src[q]);
             }
         } else if (bytes % 4 == 0 && (((uintptr_t)out_span) & 3u) == 0) {
             uint32_t* o = (uint32_t*)out_span;

@@ -134,14 +134,14 @@ template <class G>
 __device__ __forceinline__ void emit_legal(uint8_t* legal, int64_t row, uint64_t lg)
 {
 #pragma unroll
-    for (int k = 0; k < G::LB; k++) legal[row * G::LB + k] = (uint8_t)(lg >> (8 * k));
+    for (int k = 0; k < G::LB; k++) out_store(legal + row * G::LB + k, (uint8_t)(lg >> (8 * k)));
 }
 
 template <class G>
 __device__ __forceinline__ void emit_reward(float* reward, int64_t row, const float (&r)[G::P])
 {
     if constexpr (G::P == 2) {
-        *(float2*)(reward + row * 2) = make_float2(r[0], r[1]);
+        out_store((uint64_t*)(reward + row * 2), (uint64_t)__float_as_uint(r[0]) | (uint64_t)__float_as_uint(r[1]) << 32);
     } else {
 #pragma unroll
         for (int k = 0; k < G::P; k++) reward[row * G::P + k] = r[k];
@@ -500,10 +500,10 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
             const int64_t row = rowbase + c.env;
 #ifndef CS_PROF_NO_SMALL
             emit_legal<G>(legal, row, lg);
-            player[row] = (uint8_t)p;
+            out_store(player + row, (uint8_t)p);
 #endif
-            if constexpr (G::ACTION_BYTES == 1) ((uint8_t*)out.action)[row] = (uint8_t)a;
-            else ((int16_t*)out.action)[row] = (int16_t)a;
+            if constexpr (G::ACTION_BYTES == 1) out_store((uint8_t*)out.action + row, (uint8_t)a);
+            else out_store((int16_t*)out.action + row, (int16_t)a);
             g.step(a, m);
             done = g.is_over();
             if (done) {
@@ -519,7 +519,7 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
             }
 #ifndef CS_PROF_NO_SMALL
             emit_reward<G>(reward, row, r);
-            done_o[row] = (uint8_t)done;
+            out_store(done_o + row, (uint8_t)done);
 #endif
             if constexpr (DQ == 0) {
                 if (done) g.reset(m);
