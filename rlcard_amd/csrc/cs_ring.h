@@ -93,12 +93,28 @@ __device__ __forceinline__ void twist_regs(const uint32_t (&o)[10], uint32_t (&n
     }
 }
 
+// stream traffic cache policy for A/B runs: CS_RING_NT bit 0 = nontemporal loads (refill's block words, restage's
+// ring bytes), bit 1 = nontemporal stores (ring bytes, block words)
+#ifndef CS_RING_NT
+#define CS_RING_NT 0
+#endif
+__device__ __forceinline__ uint32_t ring_ld(const gu32* p)
+{
+    if constexpr ((CS_RING_NT & 1) != 0) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+__device__ __forceinline__ void ring_st(gu32* p, uint32_t v)
+{
+    if constexpr ((CS_RING_NT & 2) != 0) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // Wave-cooperative refill of one env: blocks L+1..L+3 from wbuf (block L, slot lat). All 64 lanes must call.
 __device__ __forceinline__ void ring_gen_wave(gu32* wbuf, uint32_t lat, int lane)
 {
     uint32_t o[10], n[10];
 #pragma unroll
-    for (int c = 0; c < 10; c++) o[c] = (c < 9 || lane < 48) ? wbuf[64 * c + lane] : 0u;
+    for (int c = 0; c < 10; c++) o[c] = (c < 9 || lane < 48) ? ring_ld(wbuf + 64 * c + lane) : 0u;
     gu32* ring = wbuf + MT_N;   // 624 dwords of bytes
 #pragma unroll
     for (int b = 1; b <= RING_GEN; b++) {
@@ -111,13 +127,13 @@ __device__ __forceinline__ void ring_gen_wave(gu32* wbuf, uint32_t lat, int lane
             const uint32_t t2 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x102, 0xF, 0xF, true);  // row_shl:2
             const uint32_t t3 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x103, 0xF, 0xF, true);  // row_shl:3
             if ((lane & 3) == 0 && (c < 9 || lane < 48))
-                ring[slot * (MT_N / 4) + 16 * c + (lane >> 2)] = (uint32_t)t | (t1 << 8) | (t2 << 16) | (t3 << 24);
+                ring_st(ring + slot * (MT_N / 4) + 16 * c + (lane >> 2), (uint32_t)t | (t1 << 8) | (t2 << 16) | (t3 << 24));
             o[c] = n[c];
         }
     }
 #pragma unroll
     for (int c = 0; c < 10; c++)
-        if (c < 9 || lane < 48) wbuf[64 * c + lane] = o[c];
+        if (c < 9 || lane < 48) ring_st(wbuf + 64 * c + lane, o[c]);
 }
 
 // One lane's view of its env's byte ring. MODE as MtLaneT: STAGE_NONE reads the ring in HBM per draw; STAGE_LDS
@@ -309,7 +325,7 @@ __device__ __forceinline__ void ring_restage_wave(RingLane<STAGE_LDS>& m, uint8_
                 uint32_t off = shfl(p4, s) + 4u * (uint32_t)col;
                 if (off >= RING) off -= RING;
                 const gu32* rp = (const gu32*)(uintptr_t)rb;
-                v[b] = rp[off >> 2];
+                v[b] = ring_ld(rp + (off >> 2));
             }
 #pragma unroll
             for (int b = 0; b < B; b++) *(uint32_t*)(area + src[b] * STRIDE + 4 * col) = v[b];
