@@ -14,13 +14,25 @@
 // (lane-interleaved words, so uniform word indices are bank-conflict free) because dealing indexes them dynamically.
 // "deck.pop(idx)" is an order-statistic removal: a 52-bit removed mask over the shuffled positions; the idx-th
 // remaining card is the idx-th clear bit.
+// The shuffle is not applied to a deck in memory (51 dependent LDS byte swaps per game were the kernel's critical
+// path): its draws are kept, and the card at a final deck position is found by undoing the swaps from the last one
+// back (~5 vector ops per swap, in registers) -- only the ~6 positions a game deals are ever looked up.
 // Packed state, 32 u32 words per env (word-major [32][N]):
-//   0..12  shuffled deck, card id (S,H,D,C x A..K) per byte
+//   0..12  the shuffle's draws: byte k = j of Fisher-Yates swap k (positions 51 - k and j); card id = sorted position
 //   13     removed mask bits 0..31;  14: removed bits 32..51 | deck_len << 20 | game_pointer << 26 | over << 29
 //   15..29 hands: hand h (players 0..P-1, dealer = P) bytes 12h .. 12h+11
 //   30     hand sizes 4 bits each (5 hands) | winner codes 2 bits per player << 20 (0 none, 1 tie, 2 win, 3 loss)
 #pragma once
 #include "cs_device.h"
+
+// MT staging rows of 64 bytes (a reset takes ~57 draws, so most lanes restage every step): half the LDS of 128-byte
+// rows, 3 waves per SIMD instead of 2 and half the restage passes (measured 25.5 -> 23.4 ms per 2^20 x 64 launch)
+#ifndef CS_BJ_STAGE_W
+#define CS_BJ_STAGE_W 64
+#endif
+#ifndef CS_BJ_STAGE_R
+#define CS_BJ_STAGE_R 60
+#endif
 
 namespace cs {
 
@@ -32,7 +44,7 @@ struct Blackjack {
     static constexpr bool RAW_OBS = true;      // observe() returns byte values, not a 0/1 bitmap
     static constexpr int SCRATCH_WORDS = WORDS;
     // MT staging (see MtLaneT)
-    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_PAD = 8, STAGE_R = 100;
+    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = CS_BJ_STAGE_W, STAGE_PAD = 8, STAGE_R = CS_BJ_STAGE_R;
     static constexpr int RESTAGE_B = 8;  // lanes restaged per pass (loads in flight), measured: 8 > 4 > 1
     static constexpr int MIN_WAVES = 1;  // LDS bounds the occupancy anyway
     static constexpr int EPW = 64;        // rollout envs per wave (lane_ctx)
@@ -98,15 +110,48 @@ struct Blackjack {
         return sc;
     }
 
+    // the k-th (0-based) set bit of a 64-bit mask: popcount bisection, no per-bit loop
+    __device__ static __forceinline__ int select_bit(uint64_t m, int k)
+    {
+        const uint32_t lo = (uint32_t)m;
+        const int clo = __popc(lo);
+        const bool up = k >= clo;
+        uint32_t v = up ? (uint32_t)(m >> 32) : lo;
+        k -= up ? clo : 0;
+        int base = up ? 32 : 0;
+#pragma unroll
+        for (int sh = 16; sh >= 1; sh >>= 1) {
+            const int c = __popc(v & ((1u << sh) - 1u));
+            const bool u = k >= c;
+            k -= u ? c : 0;
+            v = u ? v >> sh : v;
+            base += u ? sh : 0;
+        }
+        return base;
+    }
+    // the card at final deck position x: undo the swaps from the last (i = 1) to the first (i = 51)
+    __device__ __forceinline__ int card_at(int x) const
+    {
+        uint32_t jw[13];
+#pragma unroll
+        for (int w = 0; w < 13; w++) jw[w] = W(w);
+#pragma unroll
+        for (int i = 1; i <= 51; i++) {
+            const int k = 51 - i;
+            const int j = (int)((jw[k >> 2] >> (8 * (k & 3))) & 255u);
+            x = x == i ? j : (x == j ? i : x);
+        }
+        return x;
+    }
+
     template <class Rng>
     __device__ __forceinline__ void deal(Rng& rng, int h)
     {
         const int len = (W(14) >> 20) & 63;
         const int idx = (int)rng.interval((uint32_t)(len - 1));
-        uint64_t avail = ~((uint64_t)W(13) | (uint64_t)(W(14) & 0xFFFFFu) << 32) & ((1ull << 52) - 1);
-        for (int k = 0; k < idx; k++) avail &= avail - 1;
-        const int pos = __builtin_ctzll(avail);
-        const int c = byte_at(0, pos);
+        const uint64_t avail = ~((uint64_t)W(13) | (uint64_t)(W(14) & 0xFFFFFu) << 32) & ((1ull << 52) - 1);
+        const int pos = select_bit(avail, idx);
+        const int c = card_at(pos);
         if (!infinite) {
             if (pos < 32) W(13) |= 1u << pos;
             else W(14) |= 1u << (pos - 32);
@@ -129,15 +174,15 @@ struct Blackjack {
     template <class Rng>
     __device__ __forceinline__ void reset(Rng& rng)
     {
-        // 52-card Fisher-Yates in the deck words (bytes), then the initial deal
+        // 52-card Fisher-Yates (i = 51..1, j = randint(0, i + 1)): its draws, four per word, then the initial deal
+        for (int w = 0; w < 13; w++) {
+            uint32_t v = 0;
 #pragma unroll
-        for (int w = 0; w < 13; w++) W(w) = (uint32_t)(4 * w) | (uint32_t)(4 * w + 1) << 8 | (uint32_t)(4 * w + 2) << 16 |
-                                            (uint32_t)(4 * w + 3) << 24;
-        for (int i = 51; i >= 1; i--) {
-            const int j = (int)rng.interval((uint32_t)i);
-            const int ci = byte_at(0, i), cj = byte_at(0, j);
-            set_byte(0, i, cj);
-            set_byte(0, j, ci);
+            for (int t = 0; t < 4; t++) {
+                const int k = 4 * w + t;
+                if (k < 51) v |= rng.interval((uint32_t)(51 - k)) << (8 * t);
+            }
+            W(w) = v;
         }
         W(13) = 0;
         W(14) = 52u << 20;
