@@ -33,6 +33,9 @@
 #ifndef CS_BJ_STAGE_R
 #define CS_BJ_STAGE_R 60
 #endif
+#ifndef CS_BJ_RESTAGE_B
+#define CS_BJ_RESTAGE_B 8   // measured with 128-byte rows: 8 > 4 > 1
+#endif
 
 namespace cs {
 
@@ -45,7 +48,7 @@ struct Blackjack {
     static constexpr int SCRATCH_WORDS = WORDS;
     // MT staging (see MtLaneT)
     static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = CS_BJ_STAGE_W, STAGE_PAD = 8, STAGE_R = CS_BJ_STAGE_R;
-    static constexpr int RESTAGE_B = 8;  // lanes restaged per pass (loads in flight), measured: 8 > 4 > 1
+    static constexpr int RESTAGE_B = CS_BJ_RESTAGE_B;  // row loads in flight per lane and restage pass
     static constexpr int MIN_WAVES = 1;  // LDS bounds the occupancy anyway
     static constexpr int EPW = 64;        // rollout envs per wave (lane_ctx)
     static constexpr int REFILL_K = 2;   // stale blocks twisted per pass (see mt_refill_wave)
