@@ -25,13 +25,14 @@
 #pragma once
 #include "cs_device.h"
 
-// MT staging rows of 64 bytes (a reset takes ~57 draws, so most lanes restage every step): half the LDS of 128-byte
-// rows, 3 waves per SIMD instead of 2 and half the restage passes (measured 25.5 -> 23.4 ms per 2^20 x 64 launch)
+// MT staging rows of 128 bytes: the reset's ~57 draws come out of one branch-free pass over them
+// (RingLane::draw_intervals); measured 17.2 ms per 2^20 x 64 launch vs 19.9 with 64-byte rows (3 waves per SIMD
+// instead of 2, but more draws past the row) and 35.0 with 256-byte rows (1 wave); R 72..112 the same
 #ifndef CS_BJ_STAGE_W
-#define CS_BJ_STAGE_W 64
+#define CS_BJ_STAGE_W 128
 #endif
 #ifndef CS_BJ_STAGE_R
-#define CS_BJ_STAGE_R 60
+#define CS_BJ_STAGE_R 100
 #endif
 #ifndef CS_BJ_RESTAGE_B
 #define CS_BJ_RESTAGE_B 8   // measured with 128-byte rows: 8 > 4 > 1
@@ -177,16 +178,10 @@ struct Blackjack {
     template <class Rng>
     __device__ __forceinline__ void reset(Rng& rng)
     {
-        // 52-card Fisher-Yates (i = 51..1, j = randint(0, i + 1)): its draws, four per word, then the initial deal
-        for (int w = 0; w < 13; w++) {
-            uint32_t v = 0;
-#pragma unroll
-            for (int t = 0; t < 4; t++) {
-                const int k = 4 * w + t;
-                if (k < 51) v |= rng.interval((uint32_t)(51 - k)) << (8 * t);
-            }
-            W(w) = v;
-        }
+        // 52-card Fisher-Yates (i = 51..1, j = randint(0, i + 1)): its draws, byte k of words 0..12 (LDS byte stores),
+        // then the initial deal
+        uint8_t* jb = (uint8_t*)s;
+        rng.draw_intervals(51u, [&](uint32_t k, uint32_t j) { jb[(k >> 2) * (WAVE * 4) + (k & 3u)] = (uint8_t)j; });
         W(13) = 0;
         W(14) = 52u << 20;
 #pragma unroll

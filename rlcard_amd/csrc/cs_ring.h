@@ -270,6 +270,38 @@ struct RingLane {
         }
         for (; i >= 1; i--) (void)interval(i);
     }
+
+    // random_interval(i) for i = hi, hi - 1, .., 1 in stream order, put(k, value of draw k): one branch-free pass over
+    // the staged bytes (per byte: extract under the mask of the current i, accept, count), interval() past their end
+    template <class F>
+    __device__ __forceinline__ void draw_intervals(uint32_t hi, F&& put)
+    {
+        uint32_t i = hi;
+        if constexpr (MODE == STAGE_LDS) {
+            const uint32_t k0 = staged_offset();
+            if (i >= 1 && k0 < sn) {
+                const uint32_t* row = (const uint32_t*)(stg + (k0 & ~3u));
+                const uint32_t sh = k0 & 3u, nd = (sn - k0) >> 2;
+                uint32_t cnt = 0, lo = row[0];
+                for (uint32_t d = 0; d < nd && i >= 1; d++) {
+                    const uint32_t hw = row[d + 1];
+                    const uint32_t x = __builtin_amdgcn_alignbyte(hw, lo, sh);
+                    lo = hw;
+#pragma unroll
+                    for (uint32_t t = 0; t < 4; t++) {
+                        const bool live = i >= 1;
+                        const uint32_t u = __builtin_amdgcn_ubfe(x, 8 * t, 32u - __builtin_clz(i | 1u));
+                        const bool acc = live && u <= i;
+                        if (acc) put(hi - i, u);
+                        cnt += live ? 1u : 0u;
+                        i -= acc ? 1u : 0u;
+                    }
+                }
+                advance_by(cnt);
+            }
+        }
+        for (; i >= 1; i--) put(hi - i, interval(i));
+    }
 };
 
 // End-of-step convergence point: the wave refills every lane that is inside its latest block. All 64 lanes call.
