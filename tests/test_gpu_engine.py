@@ -151,6 +151,24 @@ def test_rollout_matches_oracle(oracle, game, name, flags):
         assert v.rng_position(i) == ob.draws(i) % v.rng_period
 
 
+@pytest.mark.parametrize('players,decks', [(2, 1), (4, 1), (1, 0), (3, 0)])
+def test_blackjack_configs_match_oracle(oracle, players, decks):
+    """Blackjack with 2-4 players and the infinite deck (num_decks 0: a dealt card stays in the deck), step API and
+    rollout launches vs the oracle (the reference fixtures hold the default game only)."""
+    n, T = 2000 + 7, 32
+    seeds = list(range(500, 500 + n))
+    v = _vec('blackjack', n, seed=500, config={'game_num_players': players, 'game_num_decks': decks})
+    keys, lens = seeding.seed_keys(seeds)
+    ob = oracle.Batch('blackjack', n, keys, lens, num_players=players, num_decks=decks)
+    _assert_same(_np(v.reset()), ob.reset(), 'reset')
+    rng = np.random.RandomState(5)
+    for t in range(12):
+        acts = rng.randint(0, 2, size=n).astype(np.int32)
+        _assert_same(_np(v.step(torch.from_numpy(acts).cuda())), ob.step(acts), 'step %d' % t)
+    for c in range(2):
+        _assert_same(_np(v.rollout(T, policy_seed=3, t0=c * T)), ob.rollout(T, 3, c * T, 0), 'rollout %d' % c)
+
+
 @pytest.mark.parametrize('game', ['limit-holdem', 'no-limit-holdem', 'leduc-holdem'])
 def test_rollout_step_reset_interleaved(oracle, game):
     """Rollout launches, single steps and resets on the same envs: the hold'em deal queue (deals the rollout drew
