@@ -169,14 +169,17 @@ def test_blackjack_configs_match_oracle(oracle, players, decks):
         _assert_same(_np(v.rollout(T, policy_seed=3, t0=c * T)), ob.rollout(T, 3, c * T, 0), 'rollout %d' % c)
 
 
-@pytest.mark.parametrize('game', ['limit-holdem', 'no-limit-holdem', 'leduc-holdem'])
-def test_rollout_step_reset_interleaved(oracle, game):
+@pytest.mark.parametrize('game,cfg', [('limit-holdem', {}), ('no-limit-holdem', {}), ('leduc-holdem', {}),
+                                      ('no-limit-holdem', {'chips_for_each': 12, 'dealer_id': 1})])
+def test_rollout_step_reset_interleaved(oracle, game, cfg):
     """Rollout launches, single steps and resets on the same envs: the hold'em deal queue (deals the rollout drew
     ahead) is consumed by cs_step / cs_reset in stream order, and the host's stream position discounts it."""
     n, T = 1000 + 13, 24
     seeds = list(range(300, 300 + n))
-    v = _vec(game, n, seed=300)
-    ob = _oracle_batch(oracle, game, seeds)
+    v = _vec(game, n, seed=300, config=cfg)
+    keys, lens = seeding.seed_keys(seeds)
+    ob = oracle.Batch(game, n, keys, lens, chips_for_each=cfg.get('chips_for_each', 100),
+                      dealer_id=cfg.get('dealer_id', -1))
     rng = np.random.RandomState(3)
     _assert_same(_np(v.reset()), ob.reset(), 'reset')
     t0 = 0
