@@ -172,12 +172,21 @@ template <class G>
 struct StageBytes {
     static constexpr int value = StageBytesOf<G::STAGE_W, G::STAGE_PAD, G::EPW, G::STAGE_MODE == STAGE_LDS>::value;
 };
+// batch restage threshold (ring_restage_wave): the game's STAGE_RF, else its STAGE_R (restage exactly the needy lanes)
+template <class G, class = void>
+struct StageRF {
+    static constexpr int value = G::STAGE_R;
+};
+template <class G>
+struct StageRF<G, std::void_t<decltype(G::STAGE_RF)>> {
+    static constexpr int value = G::STAGE_RF;
+};
 // restage after the refill, per the game's staging mode (see MtLaneT)
 template <class G, class M>
 __device__ __forceinline__ void restage(M& m, uint8_t* area, int lane, bool valid)
 {
     if constexpr (G::STAGE_MODE == STAGE_LDS)
-        ring_restage_wave<G::STAGE_W, G::STAGE_PAD, G::STAGE_R, G::RESTAGE_B>(m, area, lane, valid);
+        ring_restage_wave<G::STAGE_W, G::STAGE_PAD, G::STAGE_R, G::RESTAGE_B, StageRF<G>::value>(m, area, lane, valid);
 }
 template <class G>
 struct Scratch {   // per-lane LDS words of games that keep state in LDS (blackjack); one word per wave otherwise

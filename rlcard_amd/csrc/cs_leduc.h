@@ -15,6 +15,9 @@
 #pragma once
 #include "cs_device.h"
 
+#ifndef CS_LEDUC_STAGE_RF
+#define CS_LEDUC_STAGE_RF 24   // measured 1.94-1.99 -> 1.90-1.91 ms (40: 1.91-1.92, 56: 1.93-1.95)
+#endif
 #ifndef CS_LEDUC_RESTAGE_B
 #define CS_LEDUC_RESTAGE_B 4
 #endif
@@ -48,6 +51,7 @@ struct Leduc {
     static constexpr int SCRATCH_WORDS = 0;
     // MT staging (see MtLaneT)
     static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = CS_LEDUC_STAGE_W, STAGE_PAD = 4, STAGE_R = CS_LEDUC_STAGE_R;
+    static constexpr int STAGE_RF = CS_LEDUC_STAGE_RF;    // batch restage threshold (ring_restage_wave)
     static constexpr int RESTAGE_B = CS_LEDUC_RESTAGE_B;  // lanes restaged per pass (loads in flight): 4 > 8 > 1
     static constexpr int MIN_WAVES = CS_LEDUC_MIN_WAVES;  // rollout waves per SIMD the register budget must allow
     static constexpr int EPW = 64;        // rollout envs per wave (lane_ctx)

@@ -326,15 +326,20 @@ __device__ __forceinline__ void ring_refill_wave(M& m, int lane)
 // rows per load instruction, B instructions in flight per pass. The needy lanes are ranked with mbcnt and a ds_permute
 // pushes each one's id to the lane of its rank, so a pass picks its rows with one bpermute (no scalar bit-scan loops).
 // All 64 lanes must call.
-template <int W, int PAD, int R, int B>
+// RF > R batches the restages: nothing happens until some lane has fewer than R bytes left, then every lane with
+// fewer than RF is restaged (fewer restage events per launch, more rows per event).
+template <int W, int PAD, int R, int B, int RF = R>
 __device__ __forceinline__ void ring_restage_wave(RingLane<STAGE_LDS>& m, uint8_t* area, int lane, bool valid)
 {
     constexpr int STRIDE = Stage<W, PAD>::STRIDE, DW = W / 4, RPI = WAVE / DW, PER = B * RPI;
     static_assert(DW <= WAVE && WAVE % DW == 0, "a staged row is copied by W / 4 lanes");
+    static_assert(RF >= R && RF <= W, "restage thresholds");
     m.stg = area + lane * STRIDE;
     const uint32_t k = m.staged_offset();
-    const bool needy = valid && (k >= m.sn || m.sn - k < (uint32_t)R);
-    const uint64_t todo = __ballot(needy);
+    const uint32_t left = k >= m.sn ? 0u : m.sn - k;
+    uint64_t todo = __ballot(valid && left < (uint32_t)R);
+    if (RF > R && todo) todo = __ballot(valid && left < (uint32_t)RF);
+    const bool needy = (todo >> lane) & 1u;
     if (todo) {
         const int count = __popcll(todo);
         const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(todo >> 32),
