@@ -25,13 +25,15 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH
 # per game: default envs per GPU (BASELINE.json configs), default fused steps per launch, packed state bytes per env
 # read + written once per launch (state words + the RNG control word), and the expected tempered-u32 MT19937 draws
 # per env-step under random play (exact acceptance rates of random_interval x random-play game lengths).
+# Fused steps per launch, measured on one box: Leduc 256 vs 128 +3 % (T >= 256), Limit / No-limit 128
+# vs 64 +2.5 / +3 %, DouDizhu 128 vs 64 -7 %.
 GAMES = {
-    'leduc-holdem': dict(envs=1 << 20, T=128, state_bytes=2 * 4 + 4, draws_per_step=2.83),
-    'limit-holdem': dict(envs=262144, T=64, state_bytes=12 * 4 + 4, draws_per_step=24.5),
+    'leduc-holdem': dict(envs=1 << 20, T=256, state_bytes=2 * 4 + 4, draws_per_step=2.83),
+    'limit-holdem': dict(envs=262144, T=128, state_bytes=12 * 4 + 4, draws_per_step=24.5),
     'blackjack': dict(envs=1 << 20, T=64, state_bytes=20 * 4 + 4, draws_per_step=57.0),
     'doudizhu': dict(envs=65536, T=64, state_bytes=20 * 4 + 4, draws_per_step=1.21),
     # not a BASELINE config; draws/step counted on the oracle (4096 envs x 256 random steps)
-    'no-limit-holdem': dict(envs=262144, T=64, state_bytes=4 * 4 + 4, draws_per_step=26.3),
+    'no-limit-holdem': dict(envs=262144, T=128, state_bytes=4 * 4 + 4, draws_per_step=26.3),
 }
 
 
