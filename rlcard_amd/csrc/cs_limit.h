@@ -37,6 +37,9 @@
 #ifndef CS_LIMIT_MIN_WAVES
 #define CS_LIMIT_MIN_WAVES 5
 #endif
+#ifndef CS_LIMIT_STAGE_RF
+#define CS_LIMIT_STAGE_RF 120   // batched restage: 2.70 -> 2.65 ms per 128-step launch (R 80 / RF 100 or 124 the same)
+#endif
 #ifndef CS_LIMIT_DQ_REGS
 #define CS_LIMIT_DQ_REGS 0
 #endif
@@ -250,6 +253,7 @@ struct Limit {
     static constexpr int SCRATCH_WORDS = 0;
     // MT staging (see MtLaneT)
     static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = CS_LIMIT_STAGE_W, STAGE_PAD = 8, STAGE_R = CS_LIMIT_STAGE_R;
+    static constexpr int STAGE_RF = CS_LIMIT_STAGE_RF;    // batch restage threshold (ring_restage_wave)
     static constexpr int RESTAGE_B = CS_LIMIT_RESTAGE_B;  // lanes restaged per pass (loads in flight)
     static constexpr int MIN_WAVES = CS_LIMIT_MIN_WAVES;  // 5 waves/SIMD: beats 4 (no spills) and 6 (40 spilled VGPRs)
     static constexpr int EPW = CS_LIMIT_EPW;   // rollout envs per wave: 262 144 envs need half-full waves (lane_ctx)
