@@ -245,11 +245,14 @@ __device__ __forceinline__ uint32_t decode_action(int32_t a, const Env& e, const
 struct WaveMt {
     uint32_t* base;
     uint32_t pos, stale;
-    // 64 tempered words from pos (lane k: word pos + k); twists the next block first if the window reaches it
+    // 64 tempered words from pos (lane k: word pos + k); twists the next block first if the window reaches it or
+    // ends exactly at its start: advance() never moves past the window, so a later crossing into the next block
+    // always finds it twisted (with `>` a window ending on the block edge left the next block stale -- the first
+    // deal after such a crossing read the block consumed 1 248 draws earlier; tests/test_gpu_refill.py)
     __device__ __forceinline__ uint32_t window(int lane)
     {
         const uint32_t end = pos < (uint32_t)MT_N ? (uint32_t)MT_N : (uint32_t)MT_WORDS;
-        if (stale && pos + WAVE > end) {
+        if (stale && pos + WAVE >= end) {
             const uint32_t cur = pos < (uint32_t)MT_N ? 0u : (uint32_t)MT_N;
             mt_twist_wave(base + cur, base + (MT_N - cur), lane);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
