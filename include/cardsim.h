@@ -177,6 +177,20 @@ int cs_set_env_state(cs_handle* h, int64_t env, const uint32_t* host_words, int3
  * Hold'em envs: the position includes the draws of the queued deals (see cs_get_env_state). */
 int cs_get_rng_ctl(cs_handle* h, int64_t env, uint32_t* host_ctl);
 
+/* Evaluator test hook: the value the hold'em kernels' showdown evaluator gives `n` 7-card hands (Hand.evaluateHand +
+ * the tie-break of compare_hands, limitholdem/utils.py:3-614): cards int8 [n][7] card2index ids (suit * 13 + rank,
+ * S H D C x A 2 .. K; DEVICE), values uint32 [n] (DEVICE): category << 20 | five 4-bit tie-break ranks -- larger
+ * wins, equal splits. No handle: the evaluator is stateless. */
+int cs_debug_holdem_rank7(const int8_t* cards, int64_t n, uint32_t* values, void* stream);
+
+/* DouDizhu legal-set test hook: the legal-action bitmask the step / rollout kernels build, for `n` (hand, previous
+ * play) cases: counts u8 [n][15] (cards per rank 3 .. A, 2, black joker, red joker), prev i32 [n] (the largest play
+ * on the table, made by another player; < 0 = leading) -> legal u8 [n][3434] (bit = id, pass included when
+ * following). All DEVICE memory. Replaces Judger.playable_cards_from_hand (doudizhu/judger.py:124-258) /
+ * get_gt_cards (doudizhu/utils.py:225-262). Needs a doudizhu handle (its action table). */
+int cs_debug_ddz_legal(cs_handle* h, const uint8_t* counts, const int32_t* prev, int64_t n, uint8_t* legal,
+                       void* stream);
+
 /* Testing hook: when enabled, the wave-cooperative MT refill is skipped, so every block crossing takes the in-lane
  * serial twist; results must be identical. */
 int cs_debug_set_serial_refill(cs_handle* h, int32_t enable);

@@ -302,6 +302,26 @@ int cs_get_rng_ctl(cs_handle* h, int64_t env, uint32_t* host_ctl)
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_get_rng_ctl");
 }
 
+int cs_debug_holdem_rank7(const int8_t* cards, int64_t n, uint32_t* values, void* stream)
+{
+    if (!cards || !values) return fail(CS_E_INVALID, "null argument");
+    if (n <= 0 || n > ((int64_t)1 << 31)) return fail(CS_E_INVALID, "n out of range");
+    hipError_t e = cs::launch_debug_rank7(cards, n, values, (hipStream_t)stream);
+    return e == hipSuccess ? CS_OK : fail_hip(e, "cs_debug_holdem_rank7");
+}
+
+int cs_debug_ddz_legal(cs_handle* h, const uint8_t* counts, const int32_t* prev, int64_t n, uint8_t* legal,
+                       void* stream)
+{
+    if (!h || !counts || !prev || !legal) return fail(CS_E_INVALID, "null argument");
+    if (h->b.game != CS_GAME_DOUDIZHU) return fail(CS_E_UNSUPPORTED, "cs_debug_ddz_legal needs a doudizhu handle");
+    if (n <= 0 || n > ((int64_t)1 << 31)) return fail(CS_E_INVALID, "n out of range");
+    int r = set_device(h);
+    if (r != CS_OK) return r;
+    hipError_t e = cs::ddz::launch_debug_legal(h->b, counts, prev, n, legal, (hipStream_t)stream);
+    return e == hipSuccess ? CS_OK : fail_hip(e, "cs_debug_ddz_legal");
+}
+
 int cs_debug_set_serial_refill(cs_handle* h, int32_t enable)
 {
     if (!h) return fail(CS_E_INVALID, "null argument");

@@ -773,6 +773,37 @@ __global__ __launch_bounds__(BLOCK, CS_DDZ_MINW) void k_rollout(uint32_t* mt, ui
     if (lane == 0) ctl[c.env] = m.pos | (m.stale << 16);
 }
 
+// Test hook (cs_debug_ddz_legal): the legal set of player 0 holding `counts` -- leading when prev < 0, else following
+// another player's play `prev` -- through the same cand_of / build_legal the step and rollout kernels run (reference:
+// Judger.playable_cards_from_hand, judger.py:124-258, and get_gt_cards, utils.py:225-262, pass included)
+__global__ __launch_bounds__(BLOCK) void k_debug_legal(const uint8_t* __restrict__ counts, const int32_t* __restrict__ prev,
+                                                       int64_t n, uint8_t* legal, Tab tb)
+{
+    __shared__ WaveLds lds[WPB];
+    __shared__ TabLds tl;
+    load_tab(tl, tb);
+    const Ctx c = ctx_of(n);
+    if (!c.valid) return;
+    const uint32_t k = c.lane < 15 ? counts[c.env * 15 + c.lane] : 0u;
+    uint64_t h = 0;
+#pragma unroll
+    for (int r = 0; r < 15; r++) h |= (uint64_t)(rl(k, r) & 15u) << (4 * r);
+    const int32_t pv = prev[c.env];
+    Env e;
+    e.h0 = h; e.h1 = 0; e.h2 = 0; e.q0 = 0; e.q1 = 0; e.q2 = 0;
+    e.hw0 = e.hw1 = e.hw2 = e.hw3 = e.hw4 = 0xFFFFFFFFu;
+    e.ntrace = 0;
+    e.hcnt = 0;
+    e.cur = 0;
+    e.winner = NONE;
+    const bool lead = pv < 0 || pv >= PASS;
+    e.greater = lead ? NONE : 1u;
+    e.gplay = lead ? 0u : (uint32_t)pv;
+    e.ggrp = lead ? 0u : (uint32_t)tb.gid[pv];
+    cs_step_out o{nullptr, legal, nullptr, nullptr, nullptr};
+    emit_state(e, 0u, tb, tl, lds[c.wid], c.lane, c.env, o);
+}
+
 // _cards2array of action ids (envs/doudizhu.py:136-142 get_action_feature; pass and invalid ids -> zeros), one
 // thread per id, 27 two-byte stores per 54-byte row
 __global__ __launch_bounds__(BLOCK) void k_features(const int32_t* __restrict__ ids, int64_t count, uint8_t* out, Tab tb)
@@ -792,6 +823,13 @@ hipError_t launch_features(const Buffers& b, const int32_t* ids, int64_t count, 
 {
     hipLaunchKernelGGL(k_features, dim3((unsigned)((count + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, ids, count, out,
                        *(const Tab*)b.table);
+    return hipGetLastError();
+}
+
+hipError_t launch_debug_legal(const Buffers& b, const uint8_t* counts, const int32_t* prev, int64_t n,
+                              uint8_t* legal, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_debug_legal, grid_of(n), dim3(BLOCK), 0, s, counts, prev, n, legal, *(const Tab*)b.table);
     return hipGetLastError();
 }
 

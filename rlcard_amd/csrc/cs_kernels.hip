@@ -693,6 +693,24 @@ int game_info(int32_t game, const cs_config* cfg, cs_game_info* info)
     default: return hipErrorInvalidValue;                        \
     }
 
+// Test hook (cs_debug_holdem_rank7): the showdown evaluator of the hold'em kernels (tally_card + holdem_rank7, the
+// functions holdem_showdown and Limit's game end call) on arbitrary 7-card hands, one thread per hand
+__global__ __launch_bounds__(BLOCK) void k_debug_rank7(const int8_t* __restrict__ cards, int64_t n, uint32_t* values)
+{
+    const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    uint64_t cnt = 0, sm = 0;
+#pragma unroll
+    for (int k = 0; k < 7; k++) tally_card((int)cards[i * 7 + k], cnt, sm);
+    values[i] = holdem_rank7(cnt, sm);
+}
+
+hipError_t launch_debug_rank7(const int8_t* cards, int64_t n, uint32_t* values, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_debug_rank7, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, cards, n, values);
+    return hipGetLastError();
+}
+
 hipError_t launch_seed(const Buffers& b, const uint32_t* keys, const int32_t* klen, int64_t first, int64_t count,
                        hipStream_t s)
 {

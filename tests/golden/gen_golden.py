@@ -21,7 +21,9 @@ Fixtures written:
   doudizhu.npz     same for doudizhu (legal ids as CSR, obs padded to 901).
   cfr.npz          CFRAgent tables (policy, average_policy, regrets; keys = obs) after K train() iterations.
   holdem_eval.npz  compare_hands winner KATs on random and category-dense 7-card deals (limitholdem/utils.py).
-  ddz_judger.npz   (hand, previous play) -> legal id sets from Judger / get_gt_cards (doudizhu/judger.py, utils.py).
+  holdem_ref_kats.npz  the reference's own compare_hands known answers (tests/utils/test_holdem_utils.py), recorded.
+  ddz_judger.npz   (hand, previous play) -> legal id sets from Judger / get_gt_cards (doudizhu/judger.py, utils.py),
+                   plus the reference test's full-deck case (tests/games/test_doudizhu_judger.py:146-156).
 
 Usage:  python tests/golden/gen_golden.py [--only NAME ...]
 """
@@ -258,12 +260,13 @@ def gen_blackjack():
 
 
 def gen_doudizhu():
-    seeds = [0, 1, 42]
+    # 8 seeds x 25 games = 200 games (~12 k events): every seed's stream runs far past its first MT block refills
+    seeds = [0, 1, 42, 7, 12941, 2 ** 33 + 1, 99991, 123456789]
     st = Stream(901, 27472, 3, csr_legal=True)
 
     def pick(rng, state, env):
         return rng.choice(sorted(state['legal_actions'].keys()))
-    drive('doudizhu', {}, seeds, 4, st, pick)
+    drive('doudizhu', {}, seeds, 25, st, pick)
     st.save(os.path.join(OUT, 'doudizhu.npz'), seeds)
     print('doudizhu.npz: %d events' % len(st.obs))
 
@@ -389,6 +392,58 @@ def gen_holdem_eval():
     print('holdem_eval.npz: %d deals' % len(rows))
 
 
+def gen_holdem_ref_kats():
+    """The reference's own compare_hands known answers (tests/utils/test_holdem_utils.py): its TestHoldemUtils cases
+    are run with compare_hands wrapped to record every (hands, winners) pair it asserts on. Hands are 7 card strings
+    or None (folded). The tests use a fifth suit letter 'B' and the odd duplicate card; suits only group cards for
+    flushes, so each hand's suits are relabelled onto S, H, D, C in order of first appearance, and hands that still
+    cannot be 7 distinct cards of a real deck are marked invalid (valid = 0) rather than dropped."""
+    import importlib.util
+    import unittest
+    path = os.path.join(REF, 'tests', 'utils', 'test_holdem_utils.py')
+    spec = importlib.util.spec_from_file_location('ref_test_holdem_utils', path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    calls = []
+    orig = mod.compare_hands
+
+    def rec(hands):
+        w = orig(hands)
+        calls.append(([None if h is None else list(h) for h in hands], list(w)))
+        return w
+    mod.compare_hands = rec
+    suite = unittest.TestLoader().loadTestsFromTestCase(mod.TestHoldemUtils)
+    with open(os.devnull, 'w') as dn:
+        res = unittest.TextTestRunner(stream=dn).run(suite)
+    m = len(calls)
+    maxp = max(len(h) for h, _ in calls)
+    cards = np.full((m, maxp, 7), -1, np.int8)
+    players = np.zeros(m, np.int8)
+    winners = np.zeros((m, maxp), np.int8)
+    valid = np.ones(m, np.uint8)
+    for i, (hands, w) in enumerate(calls):
+        players[i] = len(hands)
+        winners[i, :len(w)] = w
+        for p, h in enumerate(hands):
+            if h is None:
+                continue
+            order = []
+            for c in h:
+                if c[0] not in order:
+                    order.append(c[0])
+            if len(h) != 7 or len(order) > 4:
+                valid[i] = 0
+                continue
+            ids = [SUITS.index('SHDC'[order.index(c[0])]) * 13 + RANKS.index(c[1]) for c in h]
+            if len(set(ids)) != 7:
+                valid[i] = 0
+            cards[i, p] = ids
+    np.savez_compressed(os.path.join(OUT, 'holdem_ref_kats.npz'), cards=cards, players=players, winners=winners,
+                        valid=valid)
+    print('holdem_ref_kats.npz: %d compare_hands calls (%d usable), reference tests run %d, failures %d, errors %d'
+          % (m, int(valid.sum()), res.testsRun, len(res.failures), len(res.errors)))
+
+
 RANK_CHARS = '3456789TJQKA2BR'
 
 
@@ -456,6 +511,14 @@ def gen_ddz_judger():
         prev.append(p)
         ids.extend(sorted(ACTION_2_ID[a] for a in legal))
         ptr.append(len(ids))
+    # the reference's own full-deck case (tests/games/test_doudizhu_judger.py:146-156): all 54 cards, leading ->
+    # every one of the 27 471 card combos
+    full = '3333444455556666777788889999TTTTJJJJQQQQKKKKAAAA2222BR'
+    legal = DoudizhuJudger.playable_cards_from_hand(full)
+    hands.append(np.array([4] * 13 + [1, 1], np.uint8))
+    prev.append(-1)
+    ids.extend(sorted(ACTION_2_ID[a] for a in legal))
+    ptr.append(len(ids))
     np.savez_compressed(os.path.join(OUT, 'ddz_judger.npz'), hands=np.stack(hands), prev=np.array(prev, np.int32),
                         legal_ptr=np.array(ptr, np.int64), legal_ids=np.array(ids, np.int32))
     print('ddz_judger.npz: %d cases, %d legal ids' % (len(hands), len(ids)))
@@ -467,7 +530,8 @@ def main():
     args = ap.parse_args()
     setup_reference()
     gens = {'mt19937': gen_mt, 'leduc': gen_leduc, 'limit': gen_limit, 'blackjack': gen_blackjack,
-            'doudizhu': gen_doudizhu, 'nolimit': gen_nolimit, 'cfr': gen_cfr, 'holdem_eval': gen_holdem_eval, 'ddz_table': gen_ddz_table,
+            'doudizhu': gen_doudizhu, 'nolimit': gen_nolimit, 'cfr': gen_cfr, 'holdem_eval': gen_holdem_eval,
+            'holdem_ref_kats': gen_holdem_ref_kats, 'ddz_table': gen_ddz_table,
             'ddz_judger': gen_ddz_judger}
     for name, fn in gens.items():
         if args.only is None or name in args.only:

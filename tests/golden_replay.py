@@ -7,8 +7,17 @@ import numpy as np
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 
 
+class Fixture(dict):
+    """A fixture's arrays, decompressed once (an NpzFile re-reads its zip member on every item access)."""
+
+    @property
+    def files(self):
+        return list(self.keys())
+
+
 def load(name):
-    return np.load(os.path.join(GOLDEN, name + '.npz'), allow_pickle=False)
+    with np.load(os.path.join(GOLDEN, name + '.npz'), allow_pickle=False) as z:
+        return Fixture({k: z[k] for k in z.files})
 
 
 def env_config(d, ei):

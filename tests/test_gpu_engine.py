@@ -11,8 +11,8 @@ pytestmark = pytest.mark.gpu
 GAMES = [('leduc-holdem', 'leduc'), ('limit-holdem', 'limit'), ('blackjack', 'blackjack'), ('doudizhu', 'doudizhu'),
          ('no-limit-holdem', 'nolimit')]
 # doudizhu runs one wave per env and its oracle scans the 27 472-id table per observation: smaller parity batches
-STEP_SIZE = {'doudizhu': (130, 40)}            # (envs, steps); default (3000, 120)
-ROLL_SIZE = {'doudizhu': (130, 24)}            # (envs, T); default (4197, 48)
+STEP_SIZE = {'doudizhu': (256, 80)}            # (envs, steps); default (3000, 120)
+ROLL_SIZE = {'doudizhu': (256, 48)}            # (envs, T); default (4197, 48)
 FULL_SIZE = {'leduc-holdem': (1 << 20, 16, 384), 'limit-holdem': (262144, 16, 384), 'blackjack': (262144, 16, 384),
              'doudizhu': (65536, 8, 64), 'no-limit-holdem': (262144, 16, 384)}      # (envs, T, oracle window)
 
