@@ -2,14 +2,22 @@
 
 Envs are independent, so the data path has no collective: rank r runs envs [r*N, (r+1)*N) with the
 seeds (seed + global index) and policy counters (global index) a single GPU would use for the same envs, so every
-env's trajectory is bit-identical whatever the GPU count. The only exchange is optional and happens after a rollout:
-gathering the trajectory shards (obs, legal, player, action, reward, done) to every rank with one all-gather per
-tensor (RCCL over xGMI with the nccl backend; gloo in the CPU tests).
+env's trajectory is bit-identical whatever the GPU count. The only exchange happens after a rollout, when the
+consumer wants the trajectory shards in one place:
+
+* gather_traj_to(..., dst=0): every shard to one rank (point-to-point sends into rank dst's [world, T, N, ...]
+  buffers; RCCL over xGMI with the nccl backend). xGMI is point-to-point, so rank dst receives the 7 shards over its
+  7 links at once, and no other rank holds world x the trajectory (gather to the consumer).
+* gather_traj(...): all-gather into every rank (world x the trajectory per GPU; for consumers on every rank).
+
+Timing across ranks (bench.py) goes through rank_max / whole_job_rate, so the aggregation is the one the gloo
+world-size-2 test checks.
 """
 import torch
 import torch.distributed as dist
 
-__all__ = ['shard_range', 'ShardedVecEnv', 'gather_traj', 'new_gathered']
+__all__ = ['shard_range', 'ShardedVecEnv', 'gather_traj', 'gather_traj_to', 'new_gathered', 'rank_max',
+           'whole_job_rate', 'traj_bytes']
 
 
 def shard_range(envs_per_rank, rank):
@@ -18,8 +26,12 @@ def shard_range(envs_per_rank, rank):
 
 
 def new_gathered(traj, world):
-    """Receive buffers [world, *shape] for gather_traj."""
+    """Receive buffers [world, *shape] for gather_traj / gather_traj_to (on the receiving rank only)."""
     return {k: torch.empty((world,) + tuple(v.shape), dtype=v.dtype, device=v.device) for k, v in traj.items()}
+
+
+def traj_bytes(traj):
+    return sum(v.numel() * v.element_size() for v in traj.values())
 
 
 def gather_traj(traj, out, group=None):
@@ -32,6 +44,42 @@ def gather_traj(traj, out, group=None):
         else:
             dist.all_gather_into_tensor(out[k], v.contiguous(), group=group)
     return out
+
+
+def gather_traj_to(traj, out, dst=0, group=None):
+    """Every rank's trajectory shard into rank `dst`: out[k][r] = rank r's traj[k] on dst (out is ignored, and may be
+    None, elsewhere). One batch of point-to-point operations for all tensors, so the transfers from the world - 1
+    senders run concurrently. Returns out on dst, None elsewhere."""
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    ops = []
+    if rank == dst:
+        for k, v in traj.items():
+            out[k][dst].copy_(v)
+            for r in range(world):
+                if r != dst:
+                    ops.append(dist.P2POp(dist.irecv, out[k][r], r, group))
+    else:
+        for k, v in traj.items():
+            ops.append(dist.P2POp(dist.isend, v.contiguous(), dst, group))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    return out if rank == dst else None
+
+
+def rank_max(x, device=None, group=None):
+    """max over ranks of a host float (a per-rank elapsed time); x itself with one rank."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def whole_job_rate(envs_per_rank, steps_per_launch, launches, elapsed_s, world):
+    """env-steps/s of the whole job: every rank's env-steps over the slowest rank's time (weak scaling)."""
+    return world * int(envs_per_rank) * int(steps_per_launch) * int(launches) / float(elapsed_s)
 
 
 class ShardedVecEnv:

@@ -66,3 +66,49 @@ def test_two_rank_shards_gather_to_the_single_process_trajectory(oracle, game, n
         # gathered [world, T', n, ...] -> [T', world * n, ...]
         g = np.concatenate([got[k][r] for r in range(2)], axis=1)
         assert np.array_equal(g, v), k
+
+
+def _worker_rank0(rank, world, port, game, n, T, q):
+    """gather_traj_to(dst=0) + the bench's cross-rank timing: rank_max of per-rank times, whole_job_rate."""
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from rlcard_amd.shard import shard_range, gather_traj_to, new_gathered, rank_max, whole_job_rate
+        base, m = shard_range(n, rank)
+        mine = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in _oracle_traj(game, base, m, T, 1).items()}
+        out = new_gathered(mine, world) if rank == 0 else None
+        got = gather_traj_to(mine, out, dst=0)
+        elapsed = rank_max(0.5 + rank)                         # rank r "took" 0.5 + r s
+        rate = whole_job_rate(m, T, 3, elapsed, world)
+        if rank == 0:
+            q.put(({k: v.numpy() for k, v in got.items()}, elapsed, rate))
+        else:
+            assert got is None
+            q.put((None, elapsed, rate))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('game,n,T', [('leduc-holdem', 96, 24), ('doudizhu', 8, 8)])
+def test_two_rank_gather_to_rank0_and_timing(oracle, game, n, T):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    procs = [ctx.Process(target=_worker_rank0, args=(r, world, port, game, n, T, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for got, elapsed, rate in res:
+        assert elapsed == 1.5                                 # the slowest rank's time, on every rank
+        assert rate == world * n * T * 3 / 1.5                # every rank's env-steps over that time
+    got = [g for g, _, _ in res if g is not None]
+    assert len(got) == 1
+    full = _oracle_traj(game, 0, world * n, T, 1)
+    for k, v in full.items():
+        g = np.concatenate([got[0][k][r] for r in range(world)], axis=1)
+        assert np.array_equal(g, v), k
