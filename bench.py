@@ -1,16 +1,18 @@
 #!/usr/bin/env python3
 """Benchmark of the env.step hot path (BASELINE.json): env-steps/s (whole node) + achieved HBM GB/s.
 
-One bench "step" = one cs_rollout launch: T fused lockstep env steps (default Leduc 128, the others 64) of the
-uniform-random legal policy with auto-reset over every env of the rank's shard, writing the full trajectory (obs,
-legal mask, player, action, reward, done) to HBM.
+One bench "step" = one cs_rollout launch: T fused lockstep env steps (defaults per game in GAMES: Leduc 256, Limit /
+No-limit 128, DouDizhu / Blackjack 64) of the uniform-random legal policy with auto-reset over every env of the
+rank's shard, writing the full trajectory (obs, legal mask, player, action, reward, done) to HBM.
 N>1: one process per GPU (torchrun), rank r owns envs [r*N, (r+1)*N) seeded 42 + global index -- the envs are
-independent, so there is no data-path collective (weak scaling); --gather adds the optional RCCL all-gather of the
-trajectory shards (timed separately, reported under "gather").
+independent, so the timed loop has no data-path collective (weak scaling, `value`). A second timed phase adds the
+one real exchange, returning the trajectory shards to one place (--gather rank0, the default: point-to-point RCCL
+into rank 0 over xGMI; --gather all: all-gather into every rank), reported under "gather".
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--game leduc-holdem] [--envs N_PER_GPU] [--T STEPS]
 """
 import argparse
+import hashlib
 import json
 import math
 import os
@@ -21,20 +23,28 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md (chip-level parameters)
+MT_N = 624              # words per MT19937 block
 
 # per game: default envs per GPU (BASELINE.json configs), default fused steps per launch, packed state bytes per env
-# read + written once per launch (state words + the RNG control word), and the expected tempered-u32 MT19937 draws
-# per env-step under random play (exact acceptance rates of random_interval x random-play game lengths).
+# read + written once per launch (state words + the RNG control word), the expected tempered-u32 MT19937 draws per
+# env-step under random play (exact acceptance rates of random_interval x random-play game lengths), and
+# the stream geometry: draws before the first block refill and draws per refill. Lane-per-env games keep a byte ring
+# of 4 blocks, 3 generated at seeding and 3 more per refill once the lane is inside the last one (cs_ring.h:
+# needs_refill at position >= 2 x 624); DouDizhu a two-block word window that twists one block per 624 draws
+# (cs_doudizhu.hip WaveMt::window, first twist ~1 184 draws in).
 # Fused steps per launch, measured on one box: Leduc 256 vs 128 +3 % (T >= 256), Limit / No-limit 128
 # vs 64 +2.5 / +3 %, DouDizhu 128 vs 64 -7 %.
+RING = dict(first_refill=2 * MT_N, per_refill=3 * MT_N)
 GAMES = {
-    'leduc-holdem': dict(envs=1 << 20, T=256, state_bytes=2 * 4 + 4, draws_per_step=2.83),
-    'limit-holdem': dict(envs=262144, T=128, state_bytes=12 * 4 + 4, draws_per_step=24.5),
-    'blackjack': dict(envs=1 << 20, T=64, state_bytes=20 * 4 + 4, draws_per_step=57.0),
-    'doudizhu': dict(envs=65536, T=64, state_bytes=20 * 4 + 4, draws_per_step=1.21),
+    'leduc-holdem': dict(envs=1 << 20, T=256, state_bytes=2 * 4 + 4, draws_per_step=2.83, **RING),
+    'limit-holdem': dict(envs=262144, T=128, state_bytes=12 * 4 + 4, draws_per_step=24.5, **RING),
+    'blackjack': dict(envs=1 << 20, T=64, state_bytes=20 * 4 + 4, draws_per_step=57.0, **RING),
+    'doudizhu': dict(envs=65536, T=64, state_bytes=20 * 4 + 4, draws_per_step=1.21, first_refill=1184,
+                     per_refill=MT_N),
     # not a BASELINE config; draws/step counted on the oracle (4096 envs x 256 random steps)
-    'no-limit-holdem': dict(envs=262144, T=128, state_bytes=4 * 4 + 4, draws_per_step=26.3),
+    'no-limit-holdem': dict(envs=262144, T=128, state_bytes=4 * 4 + 4, draws_per_step=26.3, **RING),
 }
+TIMED_TARGET_S = 2.0     # default --steps: enough launches for >= ~2 s of timed region (box variance, SMI sampler)
 
 
 def alg_bytes_per_env_step(info, T, game):
@@ -46,49 +56,119 @@ def alg_bytes_per_env_step(info, T, game):
             + 2.0 * g['state_bytes'] / T + 8.0 * g['draws_per_step'])
 
 
-def cpu_baseline(game, budget_s=12.0):
-    """The CPU oracle (C restatement, oracle/) timed on this host, one core, on a bounded sample of the same
-    workload (same env seeds, same policy)."""
-    sys.path.insert(0, os.path.join(ROOT, 'tests'))
-    import oracle_lib
-    from rlcard_amd import seeding
-    n_s, T_s = (256, 8) if game == 'doudizhu' else (8192, 32)   # one chunk well under the budget
-    keys, lens = seeding.seed_keys(range(42, 42 + n_s))
-    b = oracle_lib.Batch(game, n_s, keys, lens)
-    b.reset()
-    steps, t0, chunk = 0, time.perf_counter(), 0
-    while True:
-        b.rollout(T_s, 5, chunk * T_s, 0)
-        steps += n_s * T_s
-        chunk += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    return dict(value=steps / el, unit='env-steps/s', cores=1, kind='port',
-                sample='%s: %d envs (seeds 42..%d) x %d lockstep steps, uniform-legal Philox policy, %.1f s, '
-                       'oracle/liboracle.so scalar C' % (game, n_s, 41 + n_s, steps // n_s, el))
+def precondition_launches(game, T):
+    """Untimed launches so that the timed ones run at the steady-state refill rate: a freshly seeded stream refills
+    nothing for its first `first_refill` draws; run until the average env has also passed two refills."""
+    g = GAMES[game]
+    return int(math.ceil((g['first_refill'] + 2 * g['per_refill']) / (g['draws_per_step'] * T)))
+
+
+def kernel_source_digest():
+    """sha256 (16 hex) of the engine's sources: a traffic profile is only reported for the kernels it measured."""
+    d = os.path.join(ROOT, 'rlcard_amd', 'csrc')
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(d)):
+        if f.endswith(('.hip', '.h', '.cpp', '.bin')) or f == 'Makefile':
+            h.update(f.encode())
+            with open(os.path.join(d, f), 'rb') as fh:
+                h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def measured_traffic(game, envs, T):
     """HBM bytes per k_rollout launch of this configuration from the committed rocprofv3 PMC profile
-    (profiles/traffic.json, written by tools/pmc_traffic.py), or None."""
+    (profiles/traffic.json, written by tools/pmc_traffic.py), or None. An entry measured on other kernel sources
+    is returned with stale=True and is not used as `traffic`."""
     try:
         with open(os.path.join(ROOT, 'profiles', 'traffic.json')) as f:
             e = json.load(f).get('%s:%d:%d' % (game, envs, T))
     except (OSError, ValueError):
         return None
+    if e is not None:
+        e = dict(e, stale=e.get('src_sha16') != kernel_source_digest())
     return e
+
+
+def _cpu_worker(game, first, n, T, budget_s, q):
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    import oracle_lib
+    from rlcard_amd import seeding
+    keys, lens = seeding.seed_keys(range(42 + first, 42 + first + n))
+    b = oracle_lib.Batch(game, n, keys, lens)
+    b.reset()
+    steps, chunk = 0, 0
+    t0 = time.perf_counter()
+    while True:
+        b.rollout(T, 5, chunk * T, first)
+        steps += n * T
+        chunk += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    q.put((steps, el))
+
+
+def cpu_cores():
+    """Host cores this process may use: the affinity set, capped by the job's CPU share where the launcher states
+    one (OMP_NUM_THREADS: 16 per GPU on the MI355X boxes, whose os.cpu_count() is the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    cap = os.environ.get('OMP_NUM_THREADS')
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
+
+
+def cpu_baseline(game, budget_s=10.0):
+    """The CPU oracle (C restatement, oracle/) on this host: one process per core, each on its own slice of the same
+    workload (env seeds 42 + global id, same Philox policy), for a bounded wall budget."""
+    import multiprocessing as mp
+    cores = cpu_cores()
+    n_s, T_s = (64, 8) if game == 'doudizhu' else (4096, 32)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_cpu_worker, args=(game, i * n_s, n_s, T_s, budget_s, q)) for i in range(cores)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=budget_s * 20 + 120) for _ in ps]
+    for p in ps:
+        p.join()
+    steps = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    return dict(value=steps / wall, unit='env-steps/s', cores=cores, kind='port',
+                sample='%s: %d processes x %d envs (seeds 42 + global id) x lockstep chunks of %d steps, '
+                       'uniform-legal Philox policy, %.1f s wall, oracle/liboracle.so scalar C, one process per '
+                       'core' % (game, cores, n_s, T_s, wall))
+
+
+def reference_cpu(game):
+    """The reference's own env.run + RandomAgent, measured in the build container by tools/ref_cpu_baseline.py (the
+    reference does not exist on the GPU box); None when that profile is absent."""
+    try:
+        with open(os.path.join(ROOT, 'profiles', 'ref_cpu_baseline.json')) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    g = d.get('games', {}).get(game)
+    if g is None:
+        return None
+    return dict(value=g['all_cores']['value'], unit='env-steps/s', cores=g['all_cores']['processes'],
+                one_core=g['one_core']['value'], env_only_one_core=g['env_only_one_core']['value'],
+                host=d['host']['cpu'], where=d['host']['machine'], date=d['date'],
+                source='profiles/ref_cpu_baseline.json (%s)' % d['script'], method=d['method'])
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--steps', type=int, default=0,
+                    help='timed launches (default: enough for ~%.0f s of timed region, at least 20)' % TIMED_TARGET_S)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--game', default='leduc-holdem', choices=sorted(GAMES))
     ap.add_argument('--envs', type=int, default=0, help='envs per GPU (default: the BASELINE config)')
     ap.add_argument('--T', type=int, default=0, help='fused env steps per launch (default: per game, GAMES)')
-    ap.add_argument('--gather', action='store_true', help='also all-gather trajectory shards over RCCL')
+    ap.add_argument('--gather', choices=('rank0', 'all', 'none'), default='rank0',
+                    help='N>1: trajectory exchange timed in a second phase (default: every shard into rank 0)')
+    ap.add_argument('--gather-steps', type=int, default=5)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-precondition', dest='precondition', action='store_false',
                     help='time from freshly seeded streams (optimistic: no MT block refills yet)')
@@ -96,7 +176,8 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from rlcard_amd.shard import ShardedVecEnv, gather_traj, new_gathered
+    from rlcard_amd.shard import (ShardedVecEnv, gather_traj, gather_traj_to, new_gathered, rank_max, traj_bytes,
+                                  whole_job_rate)
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -107,6 +188,7 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
 
     def barrier():
         if world > 1:
@@ -118,65 +200,64 @@ def main():
     env = ShardedVecEnv(game, N, rank, seed=42, device=local)   # global envs [rank*N, (rank+1)*N)
     env.reset()
     traj = env.new_traj_out(T)
-    gathered = new_gathered(traj, world) if args.gather and world > 1 else None
 
     stream = torch.cuda.current_stream()
     t_launch = 0
-    # Precondition: every env's MT19937 stream starts at position 0 after seeding, so no env refills a block until
-    # ~624 draws in; run (untimed) until each stream has crossed two blocks on average, so the timed launches see the
-    # steady-state refill rate (measured on Leduc: launches are ~15-25 % slower once the refills start).
-    pre = int(math.ceil(2 * 624 / (GAMES[game]['draws_per_step'] * T))) if args.precondition else 0
+    pre = precondition_launches(game, T) if args.precondition else 0
     for w in range(pre):
         env.rollout(T, policy_seed=5, t0=t_launch * T, out=traj)
         t_launch += 1
+    torch.cuda.synchronize()
+    w0 = time.perf_counter()
     for w in range(args.warmup):
         env.rollout(T, policy_seed=5, t0=t_launch * T, out=traj)
         t_launch += 1
     torch.cuda.synchronize()
+    steps = args.steps
+    if steps <= 0:   # same K on every rank: from the slowest rank's warm-up
+        per = rank_max((time.perf_counter() - w0) / max(1, args.warmup), dev)
+        steps = int(min(4000, max(20, math.ceil(TIMED_TARGET_S / max(per, 1e-6)))))
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
+    for k in range(steps):
         ev[k][0].record(stream)
         env.rollout(T, policy_seed=5, t0=t_launch * T, out=traj)
         ev[k][1].record(stream)
         t_launch += 1
     torch.cuda.synchronize()
     barrier()
-    elapsed = time.perf_counter() - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    elapsed = rank_max(time.perf_counter() - t0, dev)
+    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
 
     gather_info = None
-    if gathered is not None:
+    if world > 1 and args.gather != 'none':
+        # the trajectory exchange: rollout + gather per step, timed like the main loop
+        gathered = new_gathered(traj, world) if (args.gather == 'all' or rank == 0) else None
         torch.cuda.synchronize()
         barrier()
         g0 = time.perf_counter()
-        for k in range(args.steps):
+        for k in range(args.gather_steps):
             env.rollout(T, policy_seed=5, t0=t_launch * T, out=traj)
             t_launch += 1
-            gather_traj(traj, gathered)
+            if args.gather == 'all':
+                gather_traj(traj, gathered)
+            else:
+                gather_traj_to(traj, gathered, dst=0)
         torch.cuda.synchronize()
         barrier()
-        gel = time.perf_counter() - g0
-        gather_info = dict(ms_per_step=1e3 * gel / args.steps,
-                           value=world * N * T * args.steps / gel,
-                           bytes_per_rank_per_step=sum(v.numel() * v.element_size() for v in traj.values()))
-
-    if world > 1:
-        t = torch.tensor([elapsed], device='cuda', dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        if gather_info is not None:
-            t = torch.tensor([gather_info['ms_per_step']], device='cuda', dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            gather_info['ms_per_step'] = float(t.item())
-            gather_info['value'] = world * N * T * 1e3 / gather_info['ms_per_step']
+        gel = rank_max(time.perf_counter() - g0, dev)
+        gather_info = dict(mode=args.gather, collective='RCCL %s over xGMI' % (
+                               'all_gather_into_tensor' if args.gather == 'all' else 'send/recv into rank 0'),
+                           steps=args.gather_steps, ms_per_step=1e3 * gel / args.gather_steps,
+                           value=whole_job_rate(N, T, args.gather_steps, gel, world),
+                           bytes_per_rank_per_step=traj_bytes(traj))
+        del gathered
 
     if rank == 0:
-        env_steps = world * N * T * args.steps
-        value = env_steps / elapsed
+        value = whole_job_rate(N, T, steps, elapsed, world)
         B = alg_bytes_per_env_step(env.info, T, game)
         achieved = B * N * T / (kernel_ms * 1e-3) / 1e9
         line = {
@@ -184,9 +265,9 @@ def main():
             'value': value,
             'unit': 'env-steps/s',
             'n_gpus': world,
-            'steps': args.steps,
+            'steps': steps,
             'warmup': args.warmup,
-            'ms_per_step': 1e3 * elapsed / args.steps,
+            'ms_per_step': 1e3 * elapsed / steps,
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': None,
@@ -199,18 +280,23 @@ def main():
                        'parallelism': 'env-shard x%d (no data-path collective)' % world},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
-                         'alg_bytes_per_env_step': B, 'kernel_ms_per_launch': kernel_ms,
-                         'kernel': 'k_rollout<%s>' % game},
+                         'alg_bytes_per_env_step': B, 'alg_bytes_per_launch': B * N * T,
+                         'kernel_ms_per_launch': kernel_ms, 'kernel': 'k_rollout<%s>' % game},
         }
         tr = measured_traffic(game, N, T)
-        if tr is not None:   # per launch, like `achieved`; from the profile of this exact configuration
-            line['roofline']['traffic'] = tr['bytes_per_launch']
-            line['roofline']['traffic_source'] = tr['source']
-            line['roofline']['alg_bytes_per_launch'] = B * N * T
+        if tr is not None:   # per launch, like `achieved`; from the profile of this exact configuration and kernels
+            if tr['stale']:
+                line['roofline']['traffic_stale'] = '%s measured other kernel sources' % tr['source']
+            else:
+                line['roofline']['traffic'] = tr['bytes_per_launch']
+                line['roofline']['traffic_source'] = tr['source']
         if gather_info is not None:
             line['gather'] = gather_info
         if world == 1 and not args.no_cpu_baseline:
             line['cpu_baseline'] = cpu_baseline(game)
+            ref = reference_cpu(game)
+            if ref is not None:
+                line['reference_cpu'] = ref
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
