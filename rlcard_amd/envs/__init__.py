@@ -1,48 +1,31 @@
-"""rlcard's env registry (rlcard/envs/registration.py:8-89 + envs/__init__.py) for the engine's five games."""
+"""The env registry: rlcard's plugin API (rlcard/envs/registration.py:8-89, envs/__init__.py) -- register(env_id,
+'module:Class') and make(env_id, config) -- over the engine's five games. Same ids, same config defaults and the same
+ValueError messages for an unknown or a duplicate id."""
 import importlib
 
 DEFAULT_CONFIG = {'allow_step_back': False, 'seed': None}
 
-
-class EnvSpec(object):
-    def __init__(self, env_id, entry_point):
-        self.env_id = env_id
-        mod_name, class_name = entry_point.split(':')
-        self._entry_point = getattr(importlib.import_module(mod_name), class_name)
-
-    def make(self, config=DEFAULT_CONFIG):
-        return self._entry_point(config)
-
-
-class EnvRegistry(object):
-    def __init__(self):
-        self.env_specs = {}
-
-    def register(self, env_id, entry_point):
-        if env_id in self.env_specs:
-            raise ValueError('Cannot re-register env_id: {}'.format(env_id))
-        self.env_specs[env_id] = EnvSpec(env_id, entry_point)
-
-    def make(self, env_id, config=DEFAULT_CONFIG):
-        if env_id not in self.env_specs:
-            raise ValueError('Cannot find env_id: {}'.format(env_id))
-        return self.env_specs[env_id].make(config)
-
-
-registry = EnvRegistry()
+_entry_points = {}    # env_id -> 'module:Class' (resolved on make)
 
 
 def register(env_id, entry_point):
-    return registry.register(env_id, entry_point)
+    """Add an env class under env_id; ids cannot be registered twice."""
+    if env_id in _entry_points:
+        raise ValueError('Cannot re-register env_id: {}'.format(env_id))
+    module, _, cls = entry_point.partition(':')
+    if not module or not cls:
+        raise ValueError('entry_point must be "module:Class", got {!r}'.format(entry_point))
+    _entry_points[env_id] = (module, cls)
 
 
-def make(env_id, config={}):
-    """rlcard.make(env_id, config): config keys 'seed', 'allow_step_back', the game's 'game_*' keys, and (engine
-    only) 'device', the GPU the env lives on."""
-    _config = DEFAULT_CONFIG.copy()
-    for key in config:
-        _config[key] = config[key]
-    return registry.make(env_id, _config)
+def make(env_id, config=None):
+    """rlcard.make(env_id, config): an instance of the registered class, built with DEFAULT_CONFIG updated by config
+    (keys 'seed', 'allow_step_back', the game's 'game_*' keys and, engine only, 'device': the GPU the env lives on)."""
+    if env_id not in _entry_points:
+        raise ValueError('Cannot find env_id: {}'.format(env_id))
+    module, cls = _entry_points[env_id]
+    merged = dict(DEFAULT_CONFIG, **(config or {}))
+    return getattr(importlib.import_module(module), cls)(merged)
 
 
 register('blackjack', 'rlcard_amd.envs.blackjack:BlackjackEnv')
