@@ -25,10 +25,11 @@ extern "C" const unsigned char cs_ddz_blob_end[];
 namespace cs {
 namespace ddz {
 
-// Builds the device tables; returns an error message or "" on success. *dev owns one allocation.
-std::string table_create(void** dev, Tab* tab)
+// Expands the compiled table into the host image of the device tables (cnt | gid | grp | drange, one allocation's
+// layout, offsets in *off) and the scalar fields of *tab; returns an error message or "" on success. Host code only
+// (the sanitizer driver, tools/san_driver.cpp, runs it without a GPU).
+std::string table_build_host(std::vector<uint8_t>& host, size_t off[4], Tab* tab)
 {
-    *dev = nullptr;
     const size_t size = (size_t)(cs_ddz_blob_end - cs_ddz_blob);
     if (size < 16 || memcmp(cs_ddz_blob, "DDZT", 4) != 0) return "doudizhu action table missing from the library";
     uint32_t na, pass;
@@ -96,26 +97,38 @@ std::string table_create(void** dev, Tab* tab)
     // one device allocation: cnt | gid | grp | drange
     const size_t o_cnt = 0, o_gid = o_cnt + (size_t)NA * 8, o_grp = (o_gid + (size_t)NA * 2 + 255) & ~(size_t)255,
                  o_dr = o_grp + grp.size() * 4, total = o_dr + (size_t)ND * 4;
-    std::vector<uint8_t> host(total, 0);
+    host.assign(total, 0);
     memcpy(host.data() + o_cnt, cnt.data(), (size_t)NA * 8);
     memcpy(host.data() + o_gid, gid.data(), (size_t)NA * 2);
     memcpy(host.data() + o_grp, grp.data(), grp.size() * 4);
     memcpy(host.data() + o_dr, drange.data(), (size_t)ND * 4);
-    uint8_t* d = nullptr;
-    if (hipMalloc((void**)&d, total) != hipSuccess) return "hipMalloc (doudizhu action table)";
-    if (hipMemcpy(d, host.data(), total, hipMemcpyHostToDevice) != hipSuccess) {
-        (void)hipFree(d);
-        return "hipMemcpy (doudizhu action table)";
-    }
-    *dev = d;
-    tab->cnt = (const uint64_t*)(d + o_cnt);
-    tab->gid = (const uint16_t*)(d + o_gid);
-    tab->grp = (const uint32_t*)(d + o_grp);
-    tab->drange = (const uint32_t*)(d + o_dr);
+    off[0] = o_cnt; off[1] = o_gid; off[2] = o_grp; off[3] = o_dr;
     tab->ng = ng;
     tab->bomb_lo = type_lo[TYPE_BOMB];
     tab->bomb_hi = type_hi[TYPE_BOMB];
     tab->rocket = type_lo[TYPE_ROCKET];
+    return "";
+}
+
+// Builds the device tables; returns an error message or "" on success. *dev owns one allocation.
+std::string table_create(void** dev, Tab* tab)
+{
+    *dev = nullptr;
+    std::vector<uint8_t> host;
+    size_t off[4];
+    const std::string err = table_build_host(host, off, tab);
+    if (!err.empty()) return err;
+    uint8_t* d = nullptr;
+    if (hipMalloc((void**)&d, host.size()) != hipSuccess) return "hipMalloc (doudizhu action table)";
+    if (hipMemcpy(d, host.data(), host.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return "hipMemcpy (doudizhu action table)";
+    }
+    *dev = d;
+    tab->cnt = (const uint64_t*)(d + off[0]);
+    tab->gid = (const uint16_t*)(d + off[1]);
+    tab->grp = (const uint32_t*)(d + off[2]);
+    tab->drange = (const uint32_t*)(d + off[3]);
     return "";
 }
 
