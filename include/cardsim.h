@@ -168,6 +168,11 @@ int cs_cfr_train(cs_handle* h, int32_t iterations, int64_t iteration0, double* p
  * 8 + 2 slot = MT draws of the entry). Synchronous. */
 int cs_get_env_state(cs_handle* h, int64_t env, uint32_t* host_words, int32_t nwords);
 
+/* Asynchronous cs_get_env_state: the state words of env `env` copied on `stream` into dst (u32 [state_words],
+ * DEVICE memory), so a single-env host can bring them back with its step outputs in one transfer (rlcard_amd.make's
+ * Env: one packed device-to-host copy per Env.step, envs/env.py:65-86). */
+int cs_copy_env_state(cs_handle* h, int64_t env, uint32_t* dst, void* stream);
+
 /* Overwrite the packed state words of env `env` from a HOST buffer taken by cs_get_env_state: Env.step_back
  * (envs/env.py:88-108) restores the game from its history. The env's RNG stream is left where it is, as the
  * reference's np_random is not part of the restored history. Synchronous. */

@@ -272,6 +272,17 @@ int cs_get_env_state(cs_handle* h, int64_t env, uint32_t* host_words, int32_t nw
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_get_env_state");
 }
 
+int cs_copy_env_state(cs_handle* h, int64_t env, uint32_t* dst, void* stream)
+{
+    if (!h || !dst) return fail(CS_E_INVALID, "null argument");
+    if (env < 0 || env >= h->b.n) return fail(CS_E_INVALID, "bad env");
+    if (h->info.state_words > 64) return fail(CS_E_UNSUPPORTED, "state too large for cs_copy_env_state");
+    int r = set_device(h);
+    if (r != CS_OK) return r;
+    hipError_t e = cs::launch_copy_state(h->b, env, h->info.state_words, dst, (hipStream_t)stream);
+    return e == hipSuccess ? CS_OK : fail_hip(e, "cs_copy_env_state");
+}
+
 int cs_set_env_state(cs_handle* h, int64_t env, const uint32_t* host_words, int32_t nwords)
 {
     if (!h || !host_words) return fail(CS_E_INVALID, "null argument");

@@ -50,6 +50,7 @@ hipError_t launch_transitions(const Buffers& b, int32_t T, const cs_traj_out& tr
 hipError_t launch_legal_lists(const Buffers& b, int32_t lb, const uint8_t* legal, int64_t rows, int32_t* counts,
                               int64_t* offsets, int32_t* ids, void** tmp, size_t* tmp_bytes, hipStream_t s);
 hipError_t launch_onehot(const int32_t* ids, int64_t count, int32_t na, uint8_t* out, hipStream_t s);
+hipError_t launch_copy_state(const Buffers& b, int64_t env, int32_t sw, uint32_t* dst, hipStream_t s);
 hipError_t launch_debug_rank7(const int8_t* cards, int64_t n, uint32_t* values, hipStream_t s);   // cs_kernels.hip
 
 namespace ddz {   // cs_doudizhu.hip (seeding goes through the shared k_seed)

@@ -222,6 +222,21 @@ __global__ __launch_bounds__(TBLOCK) void k_onehot(const int32_t* __restrict__ i
     out[i] = ids[r] == (int32_t)(i - r * na) ? 1 : 0;
 }
 
+// one env's packed state words (word-major [sw][n] or env-major [n][sw]) into dst: cs_copy_env_state
+__global__ void k_copy_state(const uint32_t* __restrict__ st, int64_t n, int64_t env, int sw, int env_major,
+                             uint32_t* dst)
+{
+    const int w = (int)threadIdx.x;
+    if (w < sw) dst[w] = env_major ? st[env * sw + w] : st[(int64_t)w * n + env];
+}
+
+hipError_t launch_copy_state(const Buffers& b, int64_t env, int32_t sw, uint32_t* dst, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_copy_state, dim3(1), dim3(64), 0, s, b.state, b.n, env, sw, state_env_major(b.game) ? 1 : 0,
+                       dst);
+    return hipGetLastError();
+}
+
 hipError_t launch_onehot(const int32_t* ids, int64_t count, int32_t na, uint8_t* out, hipStream_t s)
 {
     const int64_t total = count * na;

@@ -5,13 +5,53 @@ get_payoffs/is_over/get_player_id/seed/timestep/action_recorder, state dicts {'o
 'raw_legal_actions', 'action_record'} with the reference's obs dtypes and shapes -- so code written against
 rlcard.make() runs unchanged. Every game rule, deal and observation is computed by the kernels; this layer only
 converts one row of the engine's outputs into the reference's Python types. Throughput belongs to VecEnv.
+
+Per Env.step the host makes one round trip: the step kernel writes the env's outputs (reward, obs, legal bitmask,
+player, done) into slices of one device buffer, cs_copy_env_state puts the packed state words (the raw_obs fields)
+after them, and a single device-to-host copy into pinned memory brings the whole record back.
 """
+import ctypes as C
 from collections import OrderedDict
 
 import numpy as np
+import torch
 
-from .. import seeding
+from .. import _abi, seeding
 from ..vec import VecEnv, legal_ids
+
+
+class _Io:
+    """One env's step record in device memory + its pinned host mirror: reward f32 [P] | state words u32 [S] |
+    obs u8 [O] | legal u8 [LB] | player u8 | done u8."""
+
+    def __init__(self, vec):
+        i = vec.info
+        P, S, O, LB = i.num_players, i.state_words, i.obs_dim, i.legal_bytes
+        self.P, self.S, self.O, self.LB = P, S, O, LB
+        self.o_words = 4 * P
+        self.o_obs = self.o_words + 4 * S
+        self.o_legal = self.o_obs + O
+        self.o_player = self.o_legal + LB
+        self.o_done = self.o_player + 1
+        total = (self.o_done + 1 + 15) // 16 * 16
+        self.dev = torch.zeros(total, dtype=torch.uint8, device=vec.device)
+        self.host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+        self.np = self.host.numpy()
+        self.act = torch.zeros(1, dtype=torch.int32, device=vec.device)
+        base = self.dev.data_ptr()
+        self.out = _abi.StepOut(C.c_void_p(base + self.o_obs), C.c_void_p(base + self.o_legal),
+                                C.c_void_p(base + self.o_player), C.c_void_p(base), C.c_void_p(base + self.o_done))
+        self.words_ptr = C.c_void_p(base + self.o_words)
+        self.act_ptr = C.c_void_p(self.act.data_ptr())
+
+    def record(self, with_reward=True):
+        h = self.np
+        out = {'obs': h[self.o_obs:self.o_obs + self.O].copy(), 'legal': h[self.o_legal:self.o_legal + self.LB].copy(),
+               'player': int(h[self.o_player]), 'done': bool(h[self.o_done])}
+        if with_reward:
+            out['reward'] = h[:self.o_words].view(np.float32).copy()
+        words = [int(w) for w in h[self.o_words:self.o_obs].view(np.uint32)]
+        return out, words
 
 
 class Env(object):
@@ -34,6 +74,8 @@ class Env(object):
         self._vec = VecEnv(self.name, 1, seeds=[0], device=config.get('device'), config=game_config)
         self.num_players = self._vec.num_players
         self.num_actions = self._vec.num_actions
+        self._io = _Io(self._vec)
+        self._words = None   # packed state words of the last record (raw_obs / get_perfect_information)
         self.timestep = 0
         self._last = None
         self._payoffs = None
@@ -41,8 +83,27 @@ class Env(object):
         self.seed(config.get('seed'))
 
     # -- rlcard Env API ----------------------------------------------------------------------------------------
+    def _call(self, kind, arg=0, with_reward=True):
+        """One engine call on the env + the packed record back to the host (a single device-to-host copy)."""
+        io, v, L = self._io, self._vec, _abi.lib()
+        with torch.cuda.device(v.device):
+            st = v._stream()
+            if kind == 'reset':
+                _abi.check(L.cs_reset(v._h, C.byref(io.out), st), 'cs_reset')
+            elif kind == 'step':
+                io.act.fill_(int(arg))
+                _abi.check(L.cs_step(v._h, io.act_ptr, C.byref(io.out), st), 'cs_step')
+            else:
+                o = _abi.StepOut(io.out.obs, io.out.legal, io.out.player, None, io.out.done)
+                _abi.check(L.cs_observe(v._h, int(arg), C.byref(o), st), 'cs_observe')
+            _abi.check(L.cs_copy_env_state(v._h, 0, io.words_ptr, st), 'cs_copy_env_state')
+            io.host.copy_(io.dev, non_blocking=True)
+            torch.cuda.current_stream(v.device).synchronize()
+        out, self._words = io.record(with_reward)
+        return out
+
     def reset(self):
-        out = self._host(self._vec.reset())
+        out = self._call('reset')
         self.action_recorder = []
         self._payoffs = None
         self._history = []
@@ -60,7 +121,7 @@ class Env(object):
             self._history.append((self._state_words(), dict(self._last), self._payoffs))
         self.timestep += 1
         self.action_recorder.append((self.get_player_id(), decoded))
-        out = self._host(self._vec.step(np.array([self._action_id(decoded)], dtype=np.int32)))
+        out = self._call('step', self._action_id(decoded))
         if out['done']:
             self._payoffs = out['reward']
         self._last = out
@@ -79,6 +140,7 @@ class Env(object):
         if gw is not None:   # hold'em: the game words only; deals already drawn ahead stay queued
             words = list(words[:gw]) + self._vec.env_state_words(0)[gw:]
         self._vec.set_env_state_words(0, words)
+        self._words = list(words)
         self._last, self._payoffs = last, payoffs
         player_id = self.get_player_id()
         return self.get_state(player_id), player_id
@@ -112,11 +174,7 @@ class Env(object):
         return int(self._last['player'])
 
     def get_state(self, player_id):
-        o = self._vec.observe(player_id)
-        out = {k: v[0].cpu().numpy() for k, v in o.items()}
-        out['player'] = int(out['player'])
-        out['done'] = bool(out['done'])
-        return self._extract_state(out, player_id)
+        return self._extract_state(self._call('observe', player_id, with_reward=False), player_id)
 
     def get_payoffs(self):
         r = self._payoffs if self._payoffs is not None else np.zeros(self.num_players, np.float32)
@@ -135,25 +193,19 @@ class Env(object):
         s = seeding.create_seed(seed)
         self._vec.seed([s])
         self._last = None
+        self._words = None
         return s
 
     def _sync_from_engine(self):
         """Re-read the env's current game from the engine after device-side work that moved it (cs_cfr_train leaves
         the last deal at its root, as the reference's traversal leaves its env after stepping every step back)."""
-        o = self._host(self._vec.observe(0))
+        o = self._call('observe', 0, with_reward=False)
         if o['player'] != 0:
-            o = self._host(self._vec.observe(o['player']))
+            o = self._call('observe', o['player'], with_reward=False)
         o['reward'] = np.zeros(self.num_players, np.float32)
         self._last, self._payoffs, self._history = o, None, []
 
     # -- engine row -> reference types ---------------------------------------------------------------------------
-    @staticmethod
-    def _host(o):
-        out = {k: v[0].cpu().numpy() for k, v in o.items()}
-        out['player'] = int(out['player'])
-        out['done'] = bool(out['done'])
-        return out
-
     def _legal_ids(self, out):
         return legal_ids(out['legal'])
 
@@ -192,4 +244,6 @@ class Env(object):
         return np.asarray(r, dtype=np.float64)
 
     def _state_words(self):
-        return self._vec.env_state_words(0)
+        if self._words is None:
+            self._words = self._vec.env_state_words(0)
+        return self._words

@@ -179,6 +179,7 @@ static void abi_host()
     EXPECT(cs_get_env_state(nullptr, 0, nullptr, 0) == CS_E_INVALID);
     EXPECT(cs_set_env_state(nullptr, 0, nullptr, 0) == CS_E_INVALID);
     EXPECT(cs_get_rng_ctl(nullptr, 0, nullptr) == CS_E_INVALID);
+    EXPECT(cs_copy_env_state(nullptr, 0, nullptr, nullptr) == CS_E_INVALID);
     EXPECT(cs_debug_holdem_rank7(nullptr, 1, nullptr, nullptr) == CS_E_INVALID);
     EXPECT(cs_debug_ddz_legal(nullptr, nullptr, nullptr, 1, nullptr, nullptr) == CS_E_INVALID);
     EXPECT(cs_debug_set_kernel_flags(nullptr, 0) == CS_E_INVALID);
