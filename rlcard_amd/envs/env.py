@@ -7,8 +7,8 @@ rlcard.make() runs unchanged. Every game rule, deal and observation is computed 
 converts one row of the engine's outputs into the reference's Python types. Throughput belongs to VecEnv.
 
 Per Env.step the host makes one round trip: the step kernel writes the env's outputs (reward, obs, legal bitmask,
-player, done) into slices of one device buffer, cs_copy_env_state puts the packed state words (the raw_obs fields)
-after them, and a single device-to-host copy into pinned memory brings the whole record back.
+player, done) and cs_copy_env_state the packed state words (the raw_obs fields) straight into one record of mapped
+host memory, on the env's own stream; one stream synchronisation later the host decodes it (_Io).
 """
 import ctypes as C
 from collections import OrderedDict
@@ -20,9 +20,28 @@ from .. import _abi, seeding
 from ..vec import VecEnv, legal_ids
 
 
+_hip = None
+
+
+def _hip_lib():
+    global _hip
+    if _hip is None:
+        _hip = C.CDLL('libamdhip64.so')
+        _hip.hipHostMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
+        _hip.hipHostGetDevicePointer.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_uint]
+        _hip.hipHostFree.argtypes = [C.c_void_p]
+        _hip.hipStreamSynchronize.argtypes = [C.c_void_p]
+    return _hip
+
+
+HIP_HOST_MALLOC_MAPPED, HIP_HOST_MALLOC_COHERENT = 0x2, 0x40000000
+
+
 class _Io:
-    """One env's step record in device memory + its pinned host mirror: reward f32 [P] | state words u32 [S] |
-    obs u8 [O] | legal u8 [LB] | player u8 | done u8."""
+    """One env's step record, written by the kernels straight into mapped (device-visible, coherent) pinned host
+    memory: reward f32 [P] | state words u32 [S] | obs u8 [O] | legal u8 [LB] | player u8 | done u8. Actions come
+    from a constant device table of every action id (the step reads actions[0] at &table[a]), so a step is two
+    launches on the env's own stream and one stream synchronisation -- no uploads, no copies."""
 
     def __init__(self, vec):
         i = vec.info
@@ -34,15 +53,43 @@ class _Io:
         self.o_player = self.o_legal + LB
         self.o_done = self.o_player + 1
         total = (self.o_done + 1 + 15) // 16 * 16
-        self.dev = torch.zeros(total, dtype=torch.uint8, device=vec.device)
-        self.host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
-        self.np = self.host.numpy()
-        self.act = torch.zeros(1, dtype=torch.int32, device=vec.device)
-        base = self.dev.data_ptr()
+        hip = _hip_lib()
+        with torch.cuda.device(vec.device):
+            self.stream = torch.cuda.Stream(vec.device)
+            self.ids = torch.arange(i.num_actions, dtype=torch.int32, device=vec.device)
+            hp, dp = C.c_void_p(), C.c_void_p()
+            if hip.hipHostMalloc(C.byref(hp), total, HIP_HOST_MALLOC_MAPPED | HIP_HOST_MALLOC_COHERENT) != 0:
+                raise _abi.CardsimError('hipHostMalloc of the step record failed')
+            self._hp = hp
+            if hip.hipHostGetDevicePointer(C.byref(dp), hp, 0) != 0:
+                raise _abi.CardsimError('hipHostGetDevicePointer of the step record failed')
+        self.np = np.frombuffer((C.c_uint8 * total).from_address(hp.value), dtype=np.uint8)
+        self.np[:] = 0
+        base = dp.value
+        self.st = C.c_void_p(self.stream.cuda_stream)
         self.out = _abi.StepOut(C.c_void_p(base + self.o_obs), C.c_void_p(base + self.o_legal),
                                 C.c_void_p(base + self.o_player), C.c_void_p(base), C.c_void_p(base + self.o_done))
+        self.obs_out = _abi.StepOut(self.out.obs, self.out.legal, self.out.player, None, self.out.done)
         self.words_ptr = C.c_void_p(base + self.o_words)
-        self.act_ptr = C.c_void_p(self.act.data_ptr())
+        self.ids_base = self.ids.data_ptr()
+
+    def act_ptr(self, a):
+        return C.c_void_p(self.ids_base + 4 * a)
+
+    def sync(self):
+        if _hip.hipStreamSynchronize(self.st) != 0:
+            raise _abi.CardsimError('hipStreamSynchronize failed: %s' % _abi.lib().cs_last_error().decode())
+
+    def close(self):
+        if getattr(self, '_hp', None) is not None and self._hp.value:
+            _hip_lib().hipHostFree(self._hp)
+            self._hp = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def record(self, with_reward=True):
         h = self.np
@@ -50,7 +97,7 @@ class _Io:
                'player': int(h[self.o_player]), 'done': bool(h[self.o_done])}
         if with_reward:
             out['reward'] = h[:self.o_words].view(np.float32).copy()
-        words = [int(w) for w in h[self.o_words:self.o_obs].view(np.uint32)]
+        words = h[self.o_words:self.o_obs].view(np.uint32).tolist()
         return out, words
 
 
@@ -84,21 +131,16 @@ class Env(object):
 
     # -- rlcard Env API ----------------------------------------------------------------------------------------
     def _call(self, kind, arg=0, with_reward=True):
-        """One engine call on the env + the packed record back to the host (a single device-to-host copy)."""
-        io, v, L = self._io, self._vec, _abi.lib()
-        with torch.cuda.device(v.device):
-            st = v._stream()
-            if kind == 'reset':
-                _abi.check(L.cs_reset(v._h, C.byref(io.out), st), 'cs_reset')
-            elif kind == 'step':
-                io.act.fill_(int(arg))
-                _abi.check(L.cs_step(v._h, io.act_ptr, C.byref(io.out), st), 'cs_step')
-            else:
-                o = _abi.StepOut(io.out.obs, io.out.legal, io.out.player, None, io.out.done)
-                _abi.check(L.cs_observe(v._h, int(arg), C.byref(o), st), 'cs_observe')
-            _abi.check(L.cs_copy_env_state(v._h, 0, io.words_ptr, st), 'cs_copy_env_state')
-            io.host.copy_(io.dev, non_blocking=True)
-            torch.cuda.current_stream(v.device).synchronize()
+        """One engine call on the env; the kernels write the record into mapped host memory (see _Io)."""
+        io, h, L = self._io, self._vec._h, _abi.lib()
+        if kind == 'step':
+            _abi.check(L.cs_step(h, io.act_ptr(arg), C.byref(io.out), io.st), 'cs_step')
+        elif kind == 'reset':
+            _abi.check(L.cs_reset(h, C.byref(io.out), io.st), 'cs_reset')
+        else:
+            _abi.check(L.cs_observe(h, int(arg), C.byref(io.obs_out), io.st), 'cs_observe')
+        _abi.check(L.cs_copy_env_state(h, 0, io.words_ptr, io.st), 'cs_copy_env_state')
+        io.sync()
         out, self._words = io.record(with_reward)
         return out
 
@@ -199,6 +241,7 @@ class Env(object):
     def _sync_from_engine(self):
         """Re-read the env's current game from the engine after device-side work that moved it (cs_cfr_train leaves
         the last deal at its root, as the reference's traversal leaves its env after stepping every step back)."""
+        torch.cuda.current_stream(self._vec.device).synchronize()   # device work was queued on the caller's stream
         o = self._call('observe', 0, with_reward=False)
         if o['player'] != 0:
             o = self._call('observe', o['player'], with_reward=False)
