@@ -1,5 +1,5 @@
 /*
- * or_leduc.c -- TEST INFRASTRUCTURE ONLY (see oracle.h). Scalar restatement of Leduc Hold'em.
+ * or_leduc.c -- TEST INFRASTRUCTURE ONLY (see oracle.h). Scalar restatement of Leduc Hold'em (2..5 players).
  *
  * Follows, line for line in behaviour:
  *   rlcard/games/leducholdem/dealer.py:4-12    6-card deck [SJ,HJ,SQ,HQ,SK,HK], shuffled at construction
@@ -15,22 +15,26 @@
 #include "or_games.h"
 
 enum { CALL = 0, RAISE = 1, FOLD = 2, CHECK = 3 };
-#define LP 2
+#define LMAXP 5                   /* 6-card deck: N hands + the public card */
 
 typedef struct {
+    int np;                       /* game_num_players (envs/env.py:33-39 -> game.py:40-44) */
     int deck[6], deck_len;
-    int hand[LP];                 /* card id: 0 SJ, 1 HJ, 2 SQ, 3 HQ, 4 SK, 5 HK  -> rank = id / 2 */
+    int hand[LMAXP];              /* card id: 0 SJ, 1 HJ, 2 SQ, 3 HQ, 4 SK, 5 HK  -> rank = id / 2 */
     int public_card;              /* -1 = None */
-    int in_chips[LP], folded[LP];
+    int in_chips[LMAXP], folded[LMAXP];
     /* LimitHoldemRound */
-    int raise_amount, allowed_raise_num, have_raised, not_raise_num, raised[LP], round_pointer;
+    int raise_amount, allowed_raise_num, have_raised, not_raise_num, raised[LMAXP], round_pointer;
     int game_pointer, round_counter;
 } leduc_env;
 
+static int l_np(const or_cfg *cfg) { return cfg && cfg->num_players > 0 ? cfg->num_players : 2; }
+
 static int l_info(const or_cfg *cfg, or_info *info)
 {
-    (void)cfg;
-    info->obs_dim = 36; info->num_actions = 4; info->num_players = LP; info->legal_bytes = 1;
+    const int np = l_np(cfg);
+    if (np < 2 || np > LMAXP) return -1;
+    info->obs_dim = 36; info->num_actions = 4; info->num_players = np; info->legal_bytes = 1;
     return 0;
 }
 static size_t l_size(const or_cfg *cfg) { (void)cfg; return sizeof(leduc_env); }
@@ -38,7 +42,7 @@ static size_t l_size(const or_cfg *cfg) { (void)cfg; return sizeof(leduc_env); }
 static int max_raised(const leduc_env *e)
 {
     int m = e->raised[0];
-    for (int i = 1; i < LP; i++) if (e->raised[i] > m) m = e->raised[i];
+    for (int i = 1; i < e->np; i++) if (e->raised[i] > m) m = e->raised[i];
     return m;
 }
 
@@ -58,20 +62,20 @@ static void start_new_round(leduc_env *e, int game_pointer, const int *raised)
     e->round_pointer = game_pointer;
     e->have_raised = 0;
     e->not_raise_num = 0;
-    for (int i = 0; i < LP; i++) e->raised[i] = raised ? raised[i] : 0;
+    for (int i = 0; i < e->np; i++) e->raised[i] = raised ? raised[i] : 0;
 }
 
 static void l_init(void *v, or_mt *rng, const or_cfg *cfg)
 {
-    (void)cfg;
     leduc_env *e = (leduc_env *)v;
     memset(e, 0, sizeof(*e));
+    const int np = e->np = l_np(cfg);
     for (int i = 0; i < 6; i++) e->deck[i] = i;
     e->deck_len = 6;
     or_shuffle_int(rng, e->deck, 6);
-    for (int i = 0; i < LP; i++) e->hand[i] = e->deck[--e->deck_len];
-    int s = (int)or_mt_interval(rng, LP - 1);
-    int b = (s + 1) % LP;
+    for (int i = 0; i < np; i++) e->hand[i] = e->deck[--e->deck_len];
+    int s = (int)or_mt_interval(rng, (uint64_t)(np - 1));   /* randint(0, N) */
+    int b = (s + 1) % np;
     e->in_chips[b] = 2;   /* big_blind */
     e->in_chips[s] = 1;   /* small_blind */
     e->public_card = -1;
@@ -101,8 +105,8 @@ static int proceed_round(leduc_env *e, int action)
     } else {
         e->not_raise_num += 1;
     }
-    e->round_pointer = (e->round_pointer + 1) % LP;
-    while (e->folded[e->round_pointer]) e->round_pointer = (e->round_pointer + 1) % LP;
+    e->round_pointer = (e->round_pointer + 1) % e->np;
+    while (e->folded[e->round_pointer]) e->round_pointer = (e->round_pointer + 1) % e->np;
     return e->round_pointer;
 }
 
@@ -113,7 +117,7 @@ static void l_step(void *v, or_mt *rng, int a)
     unsigned legal = legal_mask(e);
     if (a < 0 || a > 3 || !((legal >> a) & 1)) a = ((legal >> CHECK) & 1) ? CHECK : FOLD;  /* _decode_action */
     e->game_pointer = proceed_round(e, a);
-    if (e->not_raise_num >= LP) {                                  /* round.is_over() */
+    if (e->not_raise_num >= e->np) {                                  /* round.is_over() */
         if (e->round_counter == 0) {
             e->public_card = e->deck[--e->deck_len];
             e->raise_amount = 2 * 2;
@@ -127,7 +131,7 @@ static int l_over(const void *v)
 {
     const leduc_env *e = (const leduc_env *)v;
     int alive = 0;
-    for (int i = 0; i < LP; i++) alive += !e->folded[i];
+    for (int i = 0; i < e->np; i++) alive += !e->folded[i];
     return alive == 1 || e->round_counter >= 2;
 }
 
@@ -140,9 +144,10 @@ static void l_observe(const void *v, int player, uint8_t *obs, uint8_t *legal)
     obs[e->hand[player] / 2] = 1;
     if (e->public_card >= 0) obs[e->public_card / 2 + 3] = 1;
     int total = 0;
-    for (int i = 0; i < LP; i++) total += e->in_chips[i];
+    for (int i = 0; i < e->np; i++) total += e->in_chips[i];
     obs[e->in_chips[player] + 6] = 1;
-    obs[total - e->in_chips[player] + 21] = 1;
+    /* others' chips past the 36-slot obs (3+ players): the reference raises IndexError; this ABI sets no bit */
+    if (total - e->in_chips[player] + 21 < 36) obs[total - e->in_chips[player] + 21] = 1;
     legal[0] = (uint8_t)legal_mask(e);
 }
 
@@ -150,28 +155,29 @@ static void l_payoffs(void *v, or_mt *rng, float *out)
 {
     (void)rng;
     leduc_env *e = (leduc_env *)v;
-    int winners[LP] = {0}, fold_count = 0, alive_idx = -1, nwin = 0, total = 0;
-    for (int i = 0; i < LP; i++) {
+    const int np = e->np;
+    int winners[LMAXP] = {0}, fold_count = 0, alive_idx = -1, nwin = 0, total = 0;
+    for (int i = 0; i < np; i++) {
         if (e->folded[i]) fold_count++;
         else alive_idx = i;
     }
-    if (fold_count == LP - 1) winners[alive_idx] = 1;
-    for (int i = 0; i < LP; i++) nwin += winners[i];
-    if (nwin < 1) {
-        for (int i = 0; i < LP; i++)
+    if (fold_count == np - 1) winners[alive_idx] = 1;
+    for (int i = 0; i < np; i++) nwin += winners[i];
+    if (nwin < 1) {   /* the first player (folded or not) whose rank matches the public card */
+        for (int i = 0; i < np; i++)
             if (e->hand[i] / 2 == e->public_card / 2) { winners[i] = 1; break; }
     }
     nwin = 0;
-    for (int i = 0; i < LP; i++) nwin += winners[i];
-    if (nwin < 1) {
+    for (int i = 0; i < np; i++) nwin += winners[i];
+    if (nwin < 1) {   /* highest rank over all players, folded ones included (judger.py:46-51) */
         int mx = -1;
-        for (int i = 0; i < LP; i++) if (e->hand[i] / 2 > mx) mx = e->hand[i] / 2;
-        for (int i = 0; i < LP; i++) if (e->hand[i] / 2 == mx) winners[i] = 1;
+        for (int i = 0; i < np; i++) if (e->hand[i] / 2 > mx) mx = e->hand[i] / 2;
+        for (int i = 0; i < np; i++) if (e->hand[i] / 2 == mx) winners[i] = 1;
     }
     nwin = 0;
-    for (int i = 0; i < LP; i++) { nwin += winners[i]; total += e->in_chips[i]; }
+    for (int i = 0; i < np; i++) { nwin += winners[i]; total += e->in_chips[i]; }
     double each_win = (double)total / nwin;
-    for (int i = 0; i < LP; i++) {
+    for (int i = 0; i < np; i++) {
         double p = winners[i] ? each_win - e->in_chips[i] : -(double)e->in_chips[i];
         out[i] = (float)(p / 2.0);
     }

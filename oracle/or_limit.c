@@ -1,5 +1,5 @@
 /*
- * or_limit.c -- TEST INFRASTRUCTURE ONLY (see oracle.h). Scalar restatement of Limit Texas Hold'em (2 players).
+ * or_limit.c -- TEST INFRASTRUCTURE ONLY (see oracle.h). Scalar restatement of Limit Texas Hold'em (2..10 players).
  *
  * Follows:
  *   rlcard/utils/utils.py:34-43                 init_standard_deck: suits S,H,D,C x ranks A,2..K (= card2index order)
@@ -21,9 +21,10 @@
 #include "or_games.h"
 
 enum { CALL = 0, RAISE = 1, FOLD = 2, CHECK = 3 };
-#define HP 2
+#define HP OR_HOLDEM_MAXP
 
 typedef struct {
+    int np;                     /* game_num_players (envs/env.py:33-39 -> game.py:42-44) */
     int deck[52], deck_len;
     int hand[HP][2];
     int pub[5], npub;
@@ -35,10 +36,13 @@ typedef struct {
     int use_prev;               /* 1 only for the obs returned by init_game                   */
 } limit_env;
 
+static int h_np(const or_cfg *cfg) { return cfg && cfg->num_players > 0 ? cfg->num_players : 2; }
+
 static int h_info(const or_cfg *cfg, or_info *info)
 {
-    (void)cfg;
-    info->obs_dim = 72; info->num_actions = 4; info->num_players = HP; info->legal_bytes = 1;
+    const int np = h_np(cfg);
+    if (np < 2 || np > HP) return -1;
+    info->obs_dim = 72; info->num_actions = 4; info->num_players = np; info->legal_bytes = 1;
     return 0;
 }
 static size_t h_size(const or_cfg *cfg) { (void)cfg; return sizeof(limit_env); }
@@ -46,7 +50,7 @@ static size_t h_size(const or_cfg *cfg) { (void)cfg; return sizeof(limit_env); }
 static int max_raised(const limit_env *e)
 {
     int m = e->raised[0];
-    for (int i = 1; i < HP; i++) if (e->raised[i] > m) m = e->raised[i];
+    for (int i = 1; i < e->np; i++) if (e->raised[i] > m) m = e->raised[i];
     return m;
 }
 
@@ -65,25 +69,25 @@ static void start_new_round(limit_env *e, int gp, const int *raised)
     e->round_pointer = gp;
     e->have_raised = 0;
     e->not_raise_num = 0;
-    for (int i = 0; i < HP; i++) e->raised[i] = raised ? raised[i] : 0;
+    for (int i = 0; i < e->np; i++) e->raised[i] = raised ? raised[i] : 0;
 }
 
 static void h_init(void *v, or_mt *rng, const or_cfg *cfg)
 {
-    (void)cfg;
     limit_env *e = (limit_env *)v;
     int prev[4];
     memcpy(prev, e->raise_nums, sizeof(prev));     /* persists across games (Game object outlives init_game) */
     memset(e, 0, sizeof(*e));
+    const int np = e->np = h_np(cfg);
     for (int i = 0; i < 52; i++) e->deck[i] = i;
     e->deck_len = 52;
     or_shuffle_int(rng, e->deck, 52);
-    for (int i = 0; i < 2 * HP; i++) e->hand[i % HP][i / HP] = e->deck[--e->deck_len];
-    int s = (int)or_mt_interval(rng, HP - 1);
-    int b = (s + 1) % HP;
+    for (int i = 0; i < 2 * np; i++) e->hand[i % np][i / np] = e->deck[--e->deck_len];
+    int s = (int)or_mt_interval(rng, (uint64_t)(np - 1));   /* randint(0, N) */
+    int b = (s + 1) % np;
     e->in_chips[b] = 2;
     e->in_chips[s] = 1;
-    e->game_pointer = (b + 1) % HP;
+    e->game_pointer = (b + 1) % np;
     e->raise_amount = 2;
     e->allowed_raise_num = 4;
     start_new_round(e, e->game_pointer, e->in_chips);
@@ -114,11 +118,11 @@ static void h_step(void *v, or_mt *rng, int a)
     } else {
         e->not_raise_num += 1;
     }
-    e->round_pointer = (e->round_pointer + 1) % HP;
-    while (e->folded[e->round_pointer]) e->round_pointer = (e->round_pointer + 1) % HP;
+    e->round_pointer = (e->round_pointer + 1) % e->np;
+    while (e->folded[e->round_pointer]) e->round_pointer = (e->round_pointer + 1) % e->np;
     e->game_pointer = e->round_pointer;
     e->raise_nums[e->round_counter] = e->have_raised;
-    if (e->not_raise_num >= HP) {
+    if (e->not_raise_num >= e->np) {
         if (e->round_counter == 0) {
             for (int k = 0; k < 3; k++) e->pub[e->npub++] = e->deck[--e->deck_len];
         } else if (e->round_counter <= 2) {
@@ -134,7 +138,7 @@ static int h_over(const void *v)
 {
     const limit_env *e = (const limit_env *)v;
     int alive = 0;
-    for (int i = 0; i < HP; i++) alive += !e->folded[i];
+    for (int i = 0; i < e->np; i++) alive += !e->folded[i];
     return alive == 1 || e->round_counter >= 4;
 }
 
@@ -224,41 +228,27 @@ uint32_t or_holdem_rank7(const int8_t *cards)
 
 static void h_payoffs(void *v, or_mt *rng, float *out)
 {
-    (void)rng;
+    /* game.py:233-243: hands of folded players are None, judge_game (or_judger.c), / big_blind. With 2 players the
+     * bets are level at a showdown and no split leaves a remainder, so np_random is never drawn; with
+     * more, an odd split of a pot among tied winners draws np_random.choice. */
     limit_env *e = (limit_env *)v;
-    /* judger.py:11-43 with 2 players: hands of folded players are None; compare_hands; pot split. With two players
-     * the bets are equal at a showdown and a lone winner takes an exact multiple, so split_pot_among_players never
-     * draws from np_random here (verified in SURVEY A10). */
-    int win[HP] = {0};
-    if (e->folded[0] || e->folded[1]) {
-        win[0] = !e->folded[0];
-        win[1] = !e->folded[1];
-    } else {
-        uint32_t r[HP];
-        for (int p = 0; p < HP; p++) {
-            int8_t c[7];
-            c[0] = (int8_t)e->hand[p][0];
-            c[1] = (int8_t)e->hand[p][1];
-            for (int k = 0; k < 5; k++) c[2 + k] = (int8_t)e->pub[k];
-            r[p] = or_holdem_rank7(c);
-        }
-        win[0] = r[0] >= r[1];
-        win[1] = r[1] >= r[0];
+    uint32_t value[HP];
+    int pay[HP];
+    for (int p = 0; p < e->np; p++) {
+        value[p] = 0;
+        if (e->folded[p]) continue;
+        int8_t c[7];
+        c[0] = (int8_t)e->hand[p][0];
+        c[1] = (int8_t)e->hand[p][1];
+        for (int k = 0; k < 5; k++) c[2 + k] = (int8_t)e->pub[k];
+        value[p] = or_holdem_rank7(c);
     }
-    /* split_pots_among_players for two players, reduced: with one winner w and loser l the winner nets
-     * min(in_w, in_l) plus nothing else (the surplus of the larger bet is returned); a tie returns the bets. */
-    int a = e->in_chips[0], b = e->in_chips[1];
-    int pay[HP] = {0, 0};
-    if (win[0] && win[1]) {
-        pay[0] = 0; pay[1] = 0;
-    } else {
-        int w = win[0] ? 0 : 1, l = 1 - w;
-        int m = a < b ? a : b;
-        pay[w] = m;
-        pay[l] = -m;
-    }
-    out[0] = (float)((double)pay[0] / 2.0);
-    out[1] = (float)((double)pay[1] / 2.0);
+    int alive = 0;
+    for (int p = 0; p < e->np; p++) alive += !e->folded[p];
+    if (alive == 1)   /* compare_hands: the one hand left wins without being evaluated (the board may be short) */
+        for (int p = 0; p < e->np; p++) value[p] = e->folded[p] ? 0u : 1u;
+    or_holdem_judge(e->np, value, e->in_chips, rng, pay);
+    for (int p = 0; p < e->np; p++) out[p] = (float)((double)pay[p] / 2.0);
 }
 
 const or_game_vt or_limit_vt = {h_info, h_size, h_init, h_step, h_over, h_cur, h_observe, h_payoffs};

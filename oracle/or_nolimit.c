@@ -1,5 +1,5 @@
 /*
- * or_nolimit.c -- TEST INFRASTRUCTURE ONLY (see oracle.h). Scalar restatement of No-limit Texas Hold'em (2 players).
+ * or_nolimit.c -- TEST INFRASTRUCTURE ONLY (see oracle.h). Scalar restatement of No-limit Texas Hold'em (2..10 players).
  *
  * Follows:
  *   rlcard/games/nolimitholdem/game.py:45-56     configure: chips_for_each, dealer_id (None = drawn once, then kept:
@@ -21,8 +21,8 @@
  *   rlcard/games/nolimitholdem/round.py:167-173  is_over: not_raise_num + not_playing_num >= N
  *   rlcard/games/limitholdem/game.py:216-231     is_over: one player alive (ALIVE or ALLIN) or round_counter >= 4
  *   rlcard/games/nolimitholdem/game.py:226-236   payoffs = judger chips (NOT divided by the big blind)
- *   rlcard/games/limitholdem/judger.py:11-108    with 2 players: the winner nets min(in0, in1), ties return the bets
- *                                                (no np_random draw: shares are exact)
+ *   rlcard/games/limitholdem/judger.py:11-108    judge_game over ALIVE / ALL-IN hands (or_judger.c): side pots, odd
+ *                                                splits draw np_random.choice
  *   rlcard/envs/nolimitholdem.py:54-85           obs[54]: card one-hot (card2index), [52] my in_chips, [53] max in_chips
  * Illegal ids: the reference's fallback names Action.CHECK, which does not exist (envs/nolimitholdem.py:98-100), so it
  * raises; this ABI defines an illegal id as CHECK_CALL (always legal).
@@ -32,9 +32,10 @@
 
 enum { FOLD = 0, CHECK_CALL = 1, RAISE_HALF_POT = 2, RAISE_POT = 3, ALL_IN = 4 };
 enum { ALIVE = 0, FOLDED = 1, ALLIN = 2 };
-#define NP 2
+#define NP OR_HOLDEM_MAXP
 
 typedef struct {
+    int np;                     /* game_num_players */
     int deck[52], deck_len;
     int hand[NP][2];
     int pub[5], npub;
@@ -46,16 +47,26 @@ typedef struct {
 
 static int n_info(const or_cfg *cfg, or_info *info)
 {
-    if (cfg->num_players != NP) return -1;
+    if (cfg->num_players < 2 || cfg->num_players > NP) return -1;
     if (cfg->chips_for_each < 1 || cfg->chips_for_each > 255) return -1;
-    if (cfg->dealer_id < -1 || cfg->dealer_id >= NP) return -1;
-    info->obs_dim = 54; info->num_actions = 5; info->num_players = NP; info->legal_bytes = 1;
+    if (cfg->dealer_id < -1 || cfg->dealer_id >= cfg->num_players) return -1;
+    info->obs_dim = 54; info->num_actions = 5; info->num_players = cfg->num_players; info->legal_bytes = 1;
     return 0;
 }
 static size_t n_size(const or_cfg *cfg) { (void)cfg; return sizeof(nl_env); }
 
-static int max_raised(const nl_env *e) { return e->raised[0] > e->raised[1] ? e->raised[0] : e->raised[1]; }
-static int pot_of(const nl_env *e) { return e->in_chips[0] + e->in_chips[1]; }
+static int max_raised(const nl_env *e)
+{
+    int m = e->raised[0];
+    for (int i = 1; i < e->np; i++) if (e->raised[i] > m) m = e->raised[i];
+    return m;
+}
+static int pot_of(const nl_env *e)
+{
+    int t = 0;
+    for (int i = 0; i < e->np; i++) t += e->in_chips[i];
+    return t;
+}
 
 static void bet(nl_env *e, int p, int chips)        /* nolimitholdem/player.py:14-17 */
 {
@@ -84,25 +95,26 @@ static void n_init(void *v, or_mt *rng, const or_cfg *cfg)
     nl_env *e = (nl_env *)v;
     int dealer_plus1 = e->dealer_plus1;
     memset(e, 0, sizeof(*e));
+    const int np = e->np = cfg->num_players;
     if (cfg->dealer_id >= 0) dealer_plus1 = cfg->dealer_id + 1;
-    if (dealer_plus1 == 0) dealer_plus1 = 1 + (int)or_mt_interval(rng, NP - 1);   /* randint(0, N), before the deal */
+    if (dealer_plus1 == 0) dealer_plus1 = 1 + (int)or_mt_interval(rng, (uint64_t)(np - 1));   /* randint(0, N), before the deal */
     e->dealer_plus1 = dealer_plus1;
     const int dealer = dealer_plus1 - 1;
     for (int i = 0; i < 52; i++) e->deck[i] = i;
     e->deck_len = 52;
     or_shuffle_int(rng, e->deck, 52);
-    for (int p = 0; p < NP; p++) {
+    for (int p = 0; p < np; p++) {
         e->remained[p] = cfg->chips_for_each;
         e->status[p] = ALIVE;
     }
-    for (int i = 0; i < 2 * NP; i++) e->hand[i % NP][i / NP] = e->deck[--e->deck_len];
-    int s = (dealer + 1) % NP, b = (dealer + 2) % NP;
+    for (int i = 0; i < 2 * np; i++) e->hand[i % np][i / np] = e->deck[--e->deck_len];
+    int s = (dealer + 1) % np, b = (dealer + 2) % np;
     bet(e, b, 2);
     bet(e, s, 1);
-    e->game_pointer = (b + 1) % NP;
+    e->game_pointer = (b + 1) % np;
     e->round_pointer = e->game_pointer;              /* start_new_round(game_pointer, raised = in_chips) */
     e->not_raise_num = 0;
-    for (int p = 0; p < NP; p++) e->raised[p] = e->in_chips[p];
+    for (int p = 0; p < np; p++) e->raised[p] = e->in_chips[p];
     e->round_counter = 0;
 }
 
@@ -137,42 +149,44 @@ static void n_step(void *v, or_mt *rng, int a)
         e->status[p] = FOLDED;
     }
     if (e->remained[p] == 0 && e->status[p] != FOLDED) e->status[p] = ALLIN;
-    int rp = (p + 1) % NP;
+    const int np = e->np;
+    int rp = (p + 1) % np;
     if (e->status[p] == ALLIN) {
         e->not_playing_num += 1;
         e->not_raise_num -= 1;
     }
     if (e->status[p] == FOLDED) e->not_playing_num += 1;
-    while (e->status[rp] == FOLDED) rp = (rp + 1) % NP;
+    while (e->status[rp] == FOLDED) rp = (rp + 1) % np;
     e->round_pointer = rp;
     e->game_pointer = rp;
     /* Game.step: bypass rule and the end of a betting round */
     int bypass[NP], nby = 0;
-    for (int i = 0; i < NP; i++) { bypass[i] = e->status[i] == FOLDED || e->status[i] == ALLIN; nby += bypass[i]; }
-    if (NP - nby == 1) {
-        int last = bypass[0] ? 1 : 0;
+    for (int i = 0; i < np; i++) { bypass[i] = e->status[i] == FOLDED || e->status[i] == ALLIN; nby += bypass[i]; }
+    if (np - nby == 1) {
+        int last = 0;
+        while (bypass[last]) last++;                 /* players_in_bypass.index(0) */
         if (e->raised[last] >= max_raised(e)) { bypass[last] = 1; nby++; }
     }
-    if (e->not_raise_num + e->not_playing_num >= NP) {
-        int gp = (e->dealer_plus1 - 1 + 1) % NP;
-        if (nby < NP) while (bypass[gp]) gp = (gp + 1) % NP;
+    if (e->not_raise_num + e->not_playing_num >= np) {
+        int gp = (e->dealer_plus1 - 1 + 1) % np;
+        if (nby < np) while (bypass[gp]) gp = (gp + 1) % np;
         if (e->round_counter == 0) {
             for (int k = 0; k < 3; k++) e->pub[e->npub++] = e->deck[--e->deck_len];
-            if (nby == NP) e->round_counter += 1;
+            if (nby == np) e->round_counter += 1;
         }
         if (e->round_counter == 1) {
             e->pub[e->npub++] = e->deck[--e->deck_len];
-            if (nby == NP) e->round_counter += 1;
+            if (nby == np) e->round_counter += 1;
         }
         if (e->round_counter == 2) {
             e->pub[e->npub++] = e->deck[--e->deck_len];
-            if (nby == NP) e->round_counter += 1;
+            if (nby == np) e->round_counter += 1;
         }
         e->round_counter += 1;
         e->game_pointer = gp;
         e->round_pointer = gp;                       /* start_new_round(gp): raised = 0, not_raise_num = 0 */
         e->not_raise_num = 0;
-        e->raised[0] = e->raised[1] = 0;
+        for (int i = 0; i < np; i++) e->raised[i] = 0;
     }
 }
 
@@ -180,7 +194,7 @@ static int n_over(const void *v)
 {
     const nl_env *e = (const nl_env *)v;
     int alive = 0;
-    for (int i = 0; i < NP; i++) alive += e->status[i] == ALIVE || e->status[i] == ALLIN;
+    for (int i = 0; i < e->np; i++) alive += e->status[i] == ALIVE || e->status[i] == ALLIN;
     return alive == 1 || e->round_counter >= 4;
 }
 
@@ -194,37 +208,32 @@ static void n_observe(const void *v, int player, uint8_t *obs, uint8_t *legal)
     obs[e->hand[player][0]] = 1;
     obs[e->hand[player][1]] = 1;
     obs[52] = (uint8_t)e->in_chips[player];
-    obs[53] = (uint8_t)(e->in_chips[0] > e->in_chips[1] ? e->in_chips[0] : e->in_chips[1]);
+    int mx = 0;
+    for (int i = 0; i < e->np; i++) if (e->in_chips[i] > mx) mx = e->in_chips[i];
+    obs[53] = (uint8_t)mx;
     legal[0] = (uint8_t)legal_mask(e);
 }
 
 static void n_payoffs(void *v, or_mt *rng, float *out)
 {
-    (void)rng;
+    /* game.py:229-236: hands of ALIVE / ALL-IN players (others None), judge_game (or_judger.c), in chips */
     nl_env *e = (nl_env *)v;
-    int win[NP];
-    int in_hand0 = e->status[0] != FOLDED, in_hand1 = e->status[1] != FOLDED;
-    if (!(in_hand0 && in_hand1)) {
-        win[0] = in_hand0;
-        win[1] = in_hand1;
-    } else {
-        uint32_t r[NP];
-        for (int p = 0; p < NP; p++) {
-            int8_t c[7];
-            c[0] = (int8_t)e->hand[p][0];
-            c[1] = (int8_t)e->hand[p][1];
-            for (int k = 0; k < 5; k++) c[2 + k] = (int8_t)e->pub[k];
-            r[p] = or_holdem_rank7(c);
-        }
-        win[0] = r[0] >= r[1];
-        win[1] = r[1] >= r[0];
+    uint32_t value[NP];
+    int pay[NP], in_hand = 0;
+    for (int p = 0; p < e->np; p++) {
+        value[p] = 0;
+        if (e->status[p] == FOLDED) continue;
+        in_hand++;
+        int8_t c[7];
+        c[0] = (int8_t)e->hand[p][0];
+        c[1] = (int8_t)e->hand[p][1];
+        for (int k = 0; k < 5; k++) c[2 + k] = (int8_t)e->pub[k];
+        value[p] = or_holdem_rank7(c);
     }
-    /* split_pots_among_players with two players (see or_limit.c): the lone winner nets min(in0, in1) */
-    int a = e->in_chips[0], b = e->in_chips[1], m = a < b ? a : b;
-    int pay0 = 0;
-    if (!(win[0] && win[1])) pay0 = win[0] ? m : -m;
-    out[0] = (float)pay0;
-    out[1] = (float)-pay0;
+    if (in_hand == 1)   /* compare_hands: the one hand left wins without being evaluated (the board may be short) */
+        for (int p = 0; p < e->np; p++) value[p] = e->status[p] == FOLDED ? 0u : 1u;
+    or_holdem_judge(e->np, value, e->in_chips, rng, pay);
+    for (int p = 0; p < e->np; p++) out[p] = (float)pay[p];
 }
 
 const or_game_vt or_nolimit_vt = {n_info, n_size, n_init, n_step, n_over, n_cur, n_observe, n_payoffs};

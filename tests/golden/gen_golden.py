@@ -19,6 +19,10 @@ Fixtures written:
                    env_dealer; -1 = dealer drawn by the game).
   blackjack.npz    same for blackjack (+ the config-1 run_random.py trajectory: env seed 42, np.random.seed(42)).
   doudizhu.npz     same for doudizhu (legal ids as CSR, obs padded to 901).
+  leduc_np.npz / limit_np.npz / nolimit_np.npz   the same streams with game_num_players 3..6 (env_np per env;
+                   no-limit also short stacks for side pots). Leduc's obs raises IndexError in the reference when
+                   the others' chips pass slot 35 (envs/leducholdem.py:64): such events are recorded with obs_len -1
+                   (obs undefined there) and the game continues through Game.step, as Env.step does before it fails.
   cfr.npz          CFRAgent tables (policy, average_policy, regrets; keys = obs) after K train() iterations.
   holdem_eval.npz  compare_hands winner KATs on random and category-dense 7-card deals (limitholdem/utils.py).
   holdem_ref_kats.npz  the reference's own compare_hands known answers (tests/utils/test_holdem_utils.py), recorded.
@@ -132,8 +136,10 @@ class Stream:
         o[:ob.size] = ob.astype(np.int64)
         return o, ob.size
 
-    def add(self, env_i, game_i, kind, act, state, player, done, payoffs):
+    def add(self, env_i, game_i, kind, act, state, player, done, payoffs, obs_ok=True):
         o, n = self.obs_row(state['obs'])
+        if not obs_ok:
+            o, n = np.zeros(self.O, dtype=np.uint8), -1
         self.ev['env'].append(env_i)
         self.ev['game'].append(game_i)
         self.ev['kind'].append(kind)
@@ -150,12 +156,14 @@ class Stream:
             self.legal.append(packbits(ids, self.A))
         p = np.zeros(self.P, dtype=np.float64)
         if done:
-            p[:] = payoffs
+            p[:len(payoffs)] = payoffs
         self.payoff.append(p)
 
-    def add_final(self, game_i, states):
-        for s in states:
+    def add_final(self, game_i, states, oks=None):
+        for k, s in enumerate(states):
             o, n = self.obs_row(s['obs'])
+            if oks is not None and not oks[k]:
+                o, n = np.zeros(self.O, dtype=np.uint8), -1
             self.fin_game.append(game_i)
             self.fin_obs.append(o)
             self.fin_obs_len.append(n)
@@ -203,6 +211,75 @@ def drive(env_id, config, seeds, games, stream, pick, extra_keys=()):
                 assert nsteps < 10000
             stream.add_final(game_counter, [env.get_state(p) for p in range(env.num_players)])
             game_counter += 1
+
+
+def drive_np(env_id, cfgs, seeds, games, stream):
+    """drive() for N-player hold'em: Env.step (env.py:65-86) spelled out so that a failing _extract_state (Leduc's
+    IndexError) leaves the event recorded with obs_len -1 and the game going. Legal actions are read from the game."""
+    import random
+    import rlcard
+    game_counter = 0
+    for ei, seed in enumerate(seeds):
+        cfg = dict(cfgs[ei])
+        cfg['seed'] = int(seed)
+        env = rlcard.make(env_id, config=cfg)
+        rng = random.Random(7919 * (ei + 1) + int(seed))
+
+        def legal_ids():
+            return sorted(env.actions.index(a) if isinstance(env.actions, list) else int(a.value)
+                          for a in env.game.get_legal_actions())
+
+        def extract(st):
+            try:
+                return env._extract_state(st), True
+            except IndexError:
+                return {'obs': np.zeros(stream.O), 'legal_actions': {i: None for i in legal_ids()}}, False
+
+        for g in range(games):
+            st, player = env.game.init_game()
+            env.action_recorder = []
+            state, ok = extract(st)
+            stream.add(ei, game_counter, 0, -1, state, player, env.is_over(), None, obs_ok=ok)
+            nsteps = 0
+            while not env.is_over():
+                legal = legal_ids()
+                a = rng.choice(legal) if (env_id == 'no-limit-holdem' or rng.random() < 0.85) else rng.randrange(4)
+                act = env._decode_action(a)
+                env.timestep += 1
+                env.action_recorder.append((env.get_player_id(), act))
+                st, player = env.game.step(act)
+                state, ok = extract(st)
+                done = env.is_over()
+                stream.add(ei, game_counter, 1, a, state, player, done, env.get_payoffs() if done else None,
+                           obs_ok=ok)
+                nsteps += 1
+                assert nsteps < 10000
+            fin = []
+            for p in range(env.num_players):
+                f, ok = extract(env.game.get_state(p))
+                fin.append((f, ok))
+            stream.add_final(game_counter, [f for f, _ in fin], [ok for _, ok in fin])
+            game_counter += 1
+
+
+def gen_nplayer():
+    specs = [('leduc-holdem', 'leduc_np', 36, 4, [3, 3, 4, 4, 5, 5], [{}] * 6, 40),
+             ('limit-holdem', 'limit_np', 72, 4, [3, 3, 4, 5, 6, 6], [{}] * 6, 30),
+             ('no-limit-holdem', 'nolimit_np', 54, 5, [3, 3, 4, 4, 6, 6, 3, 4, 6],
+              [{}] * 6 + [{'chips_for_each': 10}, {'chips_for_each': 6, 'dealer_id': 2},
+                          {'chips_for_each': 20, 'dealer_id': 5}], 40)]
+    for env_id, name, O, A, nps, extra, games in specs:
+        seeds = [11 + 17 * i for i in range(len(nps))]
+        cfgs = [dict(e, game_num_players=n) for n, e in zip(nps, extra)]
+        st = Stream(O, A, max(nps))
+        drive_np(env_id, cfgs, seeds, games, st)
+        kw = dict(env_np=np.array(nps, dtype=np.int32))
+        if env_id == 'no-limit-holdem':
+            kw['env_chips'] = np.array([c.get('chips_for_each', 100) for c in cfgs], dtype=np.int32)
+            kw['env_dealer'] = np.array([c.get('dealer_id', -1) for c in cfgs], dtype=np.int32)
+        st.save(os.path.join(OUT, name + '.npz'), seeds, **kw)
+        print('%s.npz: %d events, %d with undefined obs, %d payoff rows' % (
+            name, len(st.obs), sum(1 for n in st.ev['obs_len'] if n < 0), sum(st.ev['done'])))
 
 
 def pick_holdem(rng, state, env):
@@ -532,7 +609,7 @@ def main():
     gens = {'mt19937': gen_mt, 'leduc': gen_leduc, 'limit': gen_limit, 'blackjack': gen_blackjack,
             'doudizhu': gen_doudizhu, 'nolimit': gen_nolimit, 'cfr': gen_cfr, 'holdem_eval': gen_holdem_eval,
             'holdem_ref_kats': gen_holdem_ref_kats, 'ddz_table': gen_ddz_table,
-            'ddz_judger': gen_ddz_judger}
+            'ddz_judger': gen_ddz_judger, 'nplayer': gen_nplayer}
     for name, fn in gens.items():
         if args.only is None or name in args.only:
             fn()

@@ -21,11 +21,14 @@ def load(name):
 
 
 def env_config(d, ei):
-    """Game config of fixture env ei (nolimit.npz holds one per env; the other streams use the defaults)."""
-    if 'env_chips' not in d.files:
-        return {}
-    dealer = int(d['env_dealer'][ei])
-    return {'chips_for_each': int(d['env_chips'][ei]), 'dealer_id': None if dealer < 0 else dealer}
+    """Game config of fixture env ei (nolimit*.npz / *_np.npz hold one per env; the other streams use the defaults)."""
+    c = {}
+    if 'env_np' in d.files:
+        c['game_num_players'] = int(d['env_np'][ei])
+    if 'env_chips' in d.files:
+        dealer = int(d['env_dealer'][ei])
+        c.update({'chips_for_each': int(d['env_chips'][ei]), 'dealer_id': None if dealer < 0 else dealer})
+    return c
 
 
 def config_groups(d):
@@ -66,11 +69,12 @@ def replay(d, make_env, num_actions, check_final=True):
         kind = int(d['ev_kind'][k])
         out = env.reset() if kind == 0 else env.step(int(d['ev_act'][k]))
         ctx = 'event %d (env %d game %d kind %d act %d)' % (k, ei, d['ev_game'][k], kind, d['ev_act'][k])
-        n = int(d['ev_obs_len'][k])
+        n = int(d['ev_obs_len'][k])   # -1: the reference's obs raised there (N-player Leduc), nothing to compare
         exp_obs = d['ev_obs'][k]
         got_obs = np.asarray(out['obs']).reshape(-1)
-        assert np.array_equal(got_obs[:n], exp_obs[:n]), ctx + ' obs\n%s\n%s' % (got_obs[:n], exp_obs[:n])
-        assert not got_obs[n:].any(), ctx + ' obs padding'
+        if n >= 0:
+            assert np.array_equal(got_obs[:n], exp_obs[:n]), ctx + ' obs\n%s\n%s' % (got_obs[:n], exp_obs[:n])
+            assert not got_obs[n:].any(), ctx + ' obs padding'
         exp_legal = legal_bits_of(d, k, num_actions)
         got_legal = np.asarray(out['legal']).reshape(-1)
         assert np.array_equal(got_legal, exp_legal), ctx + ' legal %s vs %s' % (
@@ -80,11 +84,14 @@ def replay(d, make_env, num_actions, check_final=True):
         assert int(np.asarray(out['done']).reshape(-1)[0]) == int(d['ev_done'][k]), ctx + ' done'
         if d['ev_done'][k]:
             got_r = np.asarray(out['reward'], dtype=np.float64).reshape(-1)
-            assert np.array_equal(got_r, d['ev_payoff'][k]), ctx + ' payoff %s vs %s' % (got_r, d['ev_payoff'][k])
+            exp_r = d['ev_payoff'][k][:len(got_r)].astype(np.float32).astype(np.float64)   # f32 rows (ABI)
+            assert np.array_equal(got_r, exp_r), ctx + ' payoff %s vs %s' % (got_r, d['ev_payoff'][k])
             if check_final:
                 for p, j in enumerate(fin_rows[int(d['ev_game'][k])]):
                     obs, _ = env.observe(p)
                     m = int(d['fin_obs_len'][j])
+                    if m < 0:
+                        continue
                     assert np.array_equal(np.asarray(obs).reshape(-1)[:m], d['fin_obs'][j][:m]), ctx + ' final obs p%d' % p
         n_checked += 1
     return n_checked
