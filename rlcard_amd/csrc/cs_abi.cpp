@@ -195,6 +195,7 @@ int cs_cfr_train(cs_handle* h, int32_t iterations, int64_t iteration0, double* p
 {
     if (!h || !policy || !average_policy || !regrets || !flags) return fail(CS_E_INVALID, "null argument");
     if (h->b.game != CS_GAME_LEDUC) return fail(CS_E_UNSUPPORTED, "cs_cfr_train supports leduc-holdem only");
+    if (h->b.num_players != 2) return fail(CS_E_UNSUPPORTED, "cs_cfr_train: 2-player leduc-holdem only");
     if (iterations < 0 || iteration0 < 0) return fail(CS_E_INVALID, "negative iteration count");
     if (!h->seeded) return fail(CS_E_STATE, "cs_cfr_train before cs_seed");
     int r = set_device(h);

@@ -34,6 +34,22 @@ hipError_t launch_observe(const Buffers& b, int32_t player, const cs_step_out& o
 hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
                           const cs_traj_out& o, hipStream_t s);
 
+// cs_holdem_n.hip: 3..6-player hold'em (Leduc 3..5), used when Buffers::num_players > 2
+bool np_supported(int32_t game, int32_t num_players);
+int np_game_info(int32_t game, int32_t num_players, cs_game_info* info);
+int64_t np_stage_bytes(int32_t game, int32_t num_players);
+hipError_t np_launch_seed(const Buffers& b, const uint32_t* keys_dev, const int32_t* klen_dev, int64_t first,
+                          int64_t count, hipStream_t s);
+hipError_t np_launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s);
+hipError_t np_launch_step(const Buffers& b, const int32_t* actions, const cs_step_out& o, hipStream_t s);
+hipError_t np_launch_observe(const Buffers& b, int32_t player, const cs_step_out& o, hipStream_t s);
+hipError_t np_launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
+                             const cs_traj_out& o, hipStream_t s);
+inline bool is_holdem_n(const Buffers& b)
+{
+    return (b.game == CS_GAME_LEDUC || b.game == CS_GAME_LIMIT || b.game == CS_GAME_NOLIMIT) && b.num_players > 2;
+}
+
 // cs_cfr.hip: chance-sampling CFR tables on Leduc (device pointers, [CFR_NI][4] fp64 + [CFR_NI] u32 flags)
 constexpr int CFR_NI = 2700;
 struct CfrTables {

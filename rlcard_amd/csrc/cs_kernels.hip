@@ -1,14 +1,8 @@
 // cs_kernels.hip -- lockstep env kernels for gfx950 (one lane = one env, one wave = 64 consecutive envs).
 //
-// Every kernel is the same skeleton over a Game type (cs_leduc.h, ...):
-//   load packed state (word-major SoA, coalesced) -> per step: observe / legal / pick / emit rows / step / payoffs /
-//   auto-reset -> wave-cooperative MT19937 refill at the step boundary -> store state.
-// Integer/branchy work: no MFMA. The bound is HBM (obs/legal/reward rows out, packed state + RNG words in/out).
-#include <type_traits>
-
-#include "cs_device.h"
-#include "cs_ring.h"
-#include "cs_engine.h"
+// The kernel skeleton (cs_skeleton.h) instantiated for the heads-up hold'em games, Blackjack and DouDizhu's seeding;
+// 3..6-player hold'em is instantiated in cs_holdem_n.hip. game_info / dispatch for the C ABI (cs_abi.cpp).
+#include "cs_skeleton.h"
 #include "cs_leduc.h"
 #include "cs_limit.h"
 #include "cs_blackjack.h"
@@ -17,620 +11,13 @@
 
 namespace cs {
 
-constexpr int BLOCK = 256;
-constexpr int WAVES_PER_BLOCK = BLOCK / WAVE;
-
-__device__ inline void mt_init_by_array(uint32_t* mt, const uint32_t* key, int klen)
-{
-    uint32_t prev = 19650218u;
-    mt[0] = prev;
-    for (int i = 1; i < MT_N; i++) {
-        prev = 1812433253u * (prev ^ (prev >> 30)) + (uint32_t)i;
-        mt[i] = prev;
-    }
-    int i = 1, j = 0;
-    prev = mt[0];
-    for (int k = MT_N; k; k--) {
-        const uint32_t v = (mt[i] ^ ((prev ^ (prev >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
-        mt[i] = v;
-        prev = v;
-        i++;
-        j++;
-        if (i >= MT_N) { mt[0] = mt[MT_N - 1]; prev = mt[0]; i = 1; }
-        if (j >= klen) j = 0;
-    }
-    for (int k = MT_N - 1; k; k--) {
-        const uint32_t v = (mt[i] ^ ((prev ^ (prev >> 30)) * 1566083941u)) - (uint32_t)i;
-        mt[i] = v;
-        prev = v;
-        i++;
-        if (i >= MT_N) { mt[0] = mt[MT_N - 1]; prev = mt[0]; i = 1; }
-    }
-    mt[0] = 0x80000000u;
-}
-
-struct LaneCtx {
-    int lane, wid;
-    int64_t env, wave_first;
-    int nvalid;
-    bool valid;
-};
-
-// EPW envs per wave (lanes >= EPW idle): 64 everywhere but the rollouts of games with too few envs to fill the chip
-// (Limit's 262 144 envs are 4 waves per SIMD at 64 per wave; half-full waves double that -- the step is latency-bound)
-template <int EPW = WAVE>
-__device__ __forceinline__ LaneCtx lane_ctx(int64_t n)
-{
-    LaneCtx c;
-    c.lane = threadIdx.x & (WAVE - 1);
-    c.wid = threadIdx.x / WAVE;
-    c.wave_first = ((int64_t)blockIdx.x * WAVES_PER_BLOCK + c.wid) * EPW;
-    c.env = c.wave_first + c.lane;
-    const int64_t left = n - c.wave_first;
-    c.nvalid = left >= EPW ? EPW : (left > 0 ? (int)left : 0);
-    c.valid = c.lane < EPW && c.env < n;
-    return c;
-}
-
-// the lane-per-env games draw from the byte ring (cs_ring.h); invalid lanes get a ring that never needs a refill
-template <int MODE = STAGE_NONE>
-__device__ __forceinline__ RingLane<MODE> ring_lane(uint32_t* mt, const uint32_t* ctl, const LaneCtx& c)
-{
-    RingLane<MODE> m;
-    if (c.valid) m.init(mt + c.env * MT_WORDS, ctl[c.env]);
-    else m.init(mt, 0u | 2u << 12);
-    return m;
-}
-
-// end-of-step refill (flag bit 0: skipped, every block crossing takes the in-lane serial path -- a test variant)
-template <class G, class M>
-__device__ __forceinline__ void refill(M& m, int lane, int flags)
-{
-    if (!(flags & 1)) ring_refill_wave(m, lane);
-}
-
-// obs rows: staged + coalesced when the row is a dword multiple, per-lane bytes otherwise
-template <class G, int ROWS = WAVE>
-__device__ __forceinline__ void emit_obs(uint32_t* lds, const uint32_t (&bits)[G::NB], uint8_t* obs, int64_t row0, int flags,
-                                         const LaneCtx& c)
-{
-    if constexpr (G::RAW_OBS && G::OBS % 2 == 0) {
-        RowWriterRaw<G::OBS, ROWS>::write(lds, bits, obs + row0 * G::OBS, c.lane, c.nvalid, !(flags & 4));
-    } else if constexpr (G::RAW_OBS) {
-        if (c.valid) {
-            uint8_t* o = obs + (row0 + c.lane) * G::OBS;
-#pragma unroll
-            for (int k = 0; k < G::OBS; k++) o[k] = (uint8_t)(bits[k >> 2] >> (8 * (k & 3)));
-        }
-    } else if constexpr (G::OBS % 4 == 0) {
-        RowWriter<G::OBS, ROWS>::write(lds, bits, obs + row0 * G::OBS, c.lane, c.nvalid, !(flags & 4));
-    } else {
-        if (c.valid) {
-            uint8_t* o = obs + (row0 + c.lane) * G::OBS;
-#pragma unroll
-            for (int k = 0; k < G::OBS; k++) o[k] = (uint8_t)((bits[k >> 5] >> (k & 31)) & 1u);
-        }
-    }
-}
-
-// one obs row straight from a lane (final observations: only the lanes whose game just ended write)
-template <class G>
-__device__ __forceinline__ void write_obs_direct(uint8_t* o, const uint32_t (&bits)[G::NB])
-{
-    if constexpr (G::RAW_OBS) {
-#pragma unroll
-        for (int k = 0; k < G::OBS; k++) o[k] = (uint8_t)(bits[k >> 2] >> (8 * (k & 3)));
-    } else if constexpr (G::OBS % 4 == 0) {
-#pragma unroll
-        for (int j = 0; j < G::OBS / 4; j++)
-            ((uint32_t*)o)[j] = RowWriter<G::OBS>::expand4(bits[j / 8] >> (4 * (j % 8)));
-    } else {
-#pragma unroll
-        for (int k = 0; k < G::OBS; k++) o[k] = (uint8_t)((bits[k >> 5] >> (k & 31)) & 1u);
-    }
-}
-
-template <class G>
-__device__ __forceinline__ void emit_legal(uint8_t* legal, int64_t row, uint64_t lg)
-{
-#pragma unroll
-    for (int k = 0; k < G::LB; k++) out_store(legal + row * G::LB + k, (uint8_t)(lg >> (8 * k)));
-}
-
-template <class G>
-__device__ __forceinline__ void emit_reward(float* reward, int64_t row, const float (&r)[G::P])
-{
-    if constexpr (G::P == 2) {
-        out_store((uint64_t*)(reward + row * 2), (uint64_t)__float_as_uint(r[0]) | (uint64_t)__float_as_uint(r[1]) << 32);
-    } else {
-#pragma unroll
-        for (int k = 0; k < G::P; k++) reward[row * G::P + k] = r[k];
-    }
-}
-
-// LDS words of a wave's obs span image: bit rows (RowWriter, dword multiples), raw byte rows (RowWriterRaw, even)
-template <class G, int ROWS>
-constexpr int obs_lds_words()
-{
-    if constexpr (!G::RAW_OBS && G::OBS % 4 == 0) return RowWriter<G::OBS, ROWS>::LDS_WORDS;
-    else if constexpr (G::RAW_OBS && G::OBS % 2 == 0) return RowWriterRaw<G::OBS, ROWS>::LDS_WORDS;
-    else return 1;
-}
-template <class G, int ROWS = WAVE>
-struct ObsLds {
-    static constexpr int WORDS = obs_lds_words<G, ROWS>();
-};
-template <int W, int PAD, int ROWS, bool LDS>
-struct StageBytesOf {
-    static constexpr int value = 16;
-};
-template <int W, int PAD, int ROWS>
-struct StageBytesOf<W, PAD, ROWS, true> {
-    static constexpr int value = Stage<W, PAD, ROWS>::BYTES;
-};
-template <class G>
-struct StageBytes {
-    static constexpr int value = StageBytesOf<G::STAGE_W, G::STAGE_PAD, G::EPW, G::STAGE_MODE == STAGE_LDS>::value;
-};
-// batch restage threshold (ring_restage_wave): the game's STAGE_RF, else its STAGE_R (restage exactly the needy lanes)
-template <class G, class = void>
-struct StageRF {
-    static constexpr int value = G::STAGE_R;
-};
-template <class G>
-struct StageRF<G, std::void_t<decltype(G::STAGE_RF)>> {
-    static constexpr int value = G::STAGE_RF;
-};
-// restage after the refill, per the game's staging mode (see MtLaneT)
-template <class G, class M>
-__device__ __forceinline__ void restage(M& m, uint8_t* area, int lane, bool valid)
-{
-    if constexpr (G::STAGE_MODE == STAGE_LDS)
-        ring_restage_wave<G::STAGE_W, G::STAGE_PAD, G::STAGE_R, G::RESTAGE_B, StageRF<G>::value>(m, area, lane, valid);
-}
-template <class G>
-struct Scratch {   // per-lane LDS words of games that keep state in LDS (blackjack); one word per wave otherwise
-    static constexpr int WORDS = G::SCRATCH_WORDS > 0 ? G::SCRATCH_WORDS * WAVE : 1;
-};
-template <class G>
-__device__ __forceinline__ uint32_t* scratch_of(uint32_t* wave_area, int lane)
-{
-    return G::SCRATCH_WORDS > 0 ? wave_area + lane : nullptr;
-}
-// ---- hold'em deal queue (cs_limit.h): q = the env's queue words, `stride` apart (state in HBM: n; LDS copy: 1) ------
-template <class G, class = void>
-struct DqOf {
-    static constexpr int value = 0, words = 0;
-    static constexpr bool regs = false;
-};
-template <class G>
-struct DqOf<G, std::void_t<decltype(G::DQ)>> {
-    static constexpr int value = G::DQ, words = G::DQ > 0 ? 1 + 2 * G::DQ : 0;
-    static constexpr bool regs = G::DQ_REGS;
-};
-
-// queue word views: DqMem = words `stride` apart (state in HBM: n; LDS copy: 1), DqRegs = the words in registers
-// (dynamic slots through select chains, so the array never goes to scratch)
-struct DqMem {
-    uint32_t* p;
-    int64_t stride;
-    __device__ __forceinline__ uint32_t get(uint32_t i) const { return p[i * stride]; }
-    __device__ __forceinline__ void set(uint32_t i, uint32_t v) { p[i * stride] = v; }
-};
-template <int NW>
-struct DqRegs {
-    uint32_t w[NW];
-    __device__ __forceinline__ uint32_t get(uint32_t i) const
-    {
-        uint32_t r = w[0];
-#pragma unroll
-        for (int k = 1; k < NW; k++) r = i == (uint32_t)k ? w[k] : r;
-        return r;
-    }
-    __device__ __forceinline__ void set(uint32_t i, uint32_t v)
-    {
-#pragma unroll
-        for (int k = 0; k < NW; k++) w[k] = i == (uint32_t)k ? v : w[k];
-    }
-};
-
-// draw the env's next deal into its queue (the caller checks for room)
-template <class G, class Rng, class Q>
-__device__ __forceinline__ void dq_push(const G& g, Rng& rng, Q& q)
-{
-    uint32_t hdr = q.get(0);
-    const uint32_t cnt = hdr & 7u, head = (hdr >> 3) & 3u, p0 = rng.pos;
-    uint32_t e0, e1;
-    g.make_deal(rng, hdr, e0, e1);
-    uint32_t d = rng.pos >= p0 ? rng.pos - p0 : rng.pos + (uint32_t)RING - p0;
-    d = d < 511u ? d : 511u;
-    const uint32_t slot = (head + cnt) & (uint32_t)(G::DQ - 1), hi = 7u + 2u * slot;
-    q.set(1 + 2 * slot, e0 | (d & 127u) << 25);
-    q.set(2 + 2 * slot, e1);
-    q.set(0, (hdr & ~7u & ~(3u << hi)) | (d >> 7) << hi | (cnt + 1u));
-}
-
-// Game.init_game: the oldest queued deal, or a deal drawn now when the queue is empty
-template <class G, class Rng, class Q>
-__device__ __forceinline__ void dq_reset(G& g, Rng& rng, Q& q)
-{
-    uint32_t hdr = q.get(0), e0, e1;
-    const uint32_t cnt = hdr & 7u, head = (hdr >> 3) & 3u;
-    if (cnt) {
-        e0 = q.get(1 + 2 * head);
-        e1 = q.get(2 + 2 * head);
-        hdr = (hdr & ~0x1Fu) | (cnt - 1u) | ((head + 1u) & (uint32_t)(G::DQ - 1)) << 3;
-    } else {
-        g.make_deal(rng, hdr, e0, e1);
-    }
-    q.set(0, hdr);
-    g.reset_from(e0, e1);
-}
-
-// reset of the env's game through its deal queue where the game has one
-template <class G, class Rng>
-__device__ __forceinline__ void game_reset(G& g, Rng& rng, uint32_t* st, int64_t n, int64_t env)
-{
-    if constexpr (DqOf<G>::value > 0) {
-        DqMem q{st + (int64_t)G::GW * n + env, n};
-        dq_reset(g, rng, q);
-    } else {
-        g.reset(rng);
-    }
-}
-
-#define CS_SMEM_ROWS(G, ROWS)                                         \
-    __shared__ uint32_t lds[WAVES_PER_BLOCK][ObsLds<G, ROWS>::WORDS]; \
-    __shared__ uint32_t scr[WAVES_PER_BLOCK][Scratch<G>::WORDS]
-#define CS_SMEM(G) CS_SMEM_ROWS(G, WAVE)
-
-// ------------------------------------------------------------------------------------------------------------------
-template <class G>
-__global__ __launch_bounds__(BLOCK) void k_seed(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
-                                                 const uint32_t* keys, const int32_t* klen, int64_t first,
-                                                 int64_t count, int flags, GameParams prm)
-{
-    __shared__ uint32_t scr[WAVES_PER_BLOCK][Scratch<G>::WORDS];
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-    const bool valid = i < count;
-    const int64_t env = first + i;
-    if constexpr (G::RING) {   // byte ring: S0 = init_by_array(key) in wbuf, blocks 0..2 generated in place
-        if (!valid) return;
-        uint32_t* wbuf = mt + env * MT_WORDS;
-        const int kl = klen[i] == 2 ? 2 : 1;                    // validated on the host; never trust it here
-        mt_init_by_array(wbuf, keys + 2 * i, kl);
-        for (uint32_t b = 0; b < (uint32_t)RING_GEN; b++) {     // numpy's first draws: block 0 = twist(S0)
-            mt_twist_inplace(wbuf);
-            ring_bytes_serial(wbuf, (uint8_t*)(wbuf + MT_N), b);
-        }
-        G g;
-        g.bind(scratch_of<G>(scr[threadIdx.x / WAVE], lane), prm);
-        g.blank();
-        g.store(st, n, env);
-        if constexpr (DqOf<G>::value > 0) st[(int64_t)G::GW * n + env] = 0u;   // empty deal queue
-        ctl[env] = 0u | (uint32_t)(RING_GEN - 1) << 12;          // position 0, latest block in slot 2
-        return;
-    }
-    MtLane m;
-    m.init(mt, 0, 0);
-    if (valid) {
-        uint32_t* base = mt + env * MT_WORDS;
-        const int kl = klen[i] == 2 ? 2 : 1;                    // validated on the host; never trust it here
-        mt_init_by_array(base + MT_N, keys + 2 * i, kl);        // S0 in block 1 (scratch)
-        mt_twist_serial(base + MT_N, base);                     // block 0 = twist(S0): numpy's first draws
-        m.base = base;
-        m.stale = 1;                                            // block 1 = twist(block 0), refilled below
-        G g;
-        g.bind(scratch_of<G>(scr[threadIdx.x / WAVE], lane), prm);
-        g.blank();
-        g.store(st, n, env);
-    }
-    if (flags & 1) {
-        if (valid) mt_twist_serial(m.base, m.base + MT_N);
-        m.stale = 0;
-    } else {
-        mt_refill_wave(m, lane);
-    }
-    if (valid) ctl[env] = 0u;
-}
-
-template <class G>
-__global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
-                                                  cs_step_out out, int flags, GameParams prm)
-{
-    CS_SMEM(G);
-    const LaneCtx c = lane_ctx(n);
-    RingLane<> m = ring_lane(mt, ctl, c);
-    G g;
-    g.bind(scratch_of<G>(scr[c.wid], c.lane), prm);
-    g.blank();
-    if (c.valid) {
-        g.load(st, n, c.env);   // the Game object outlives init_game (limit-holdem's raise history, :98/:101)
-        game_reset(g, m, st, n, c.env);
-    }
-    refill<G>(m, c.lane, flags & 1);
-    uint32_t bits[G::NB];
-    const int p = g.current();
-    g.observe(p, bits);
-    if (out.obs) emit_obs<G>(lds[c.wid], bits, (uint8_t*)out.obs, c.wave_first, flags, c);
-    if (c.valid) {
-        if (out.legal) emit_legal<G>((uint8_t*)out.legal, c.env, g.legal());
-        if (out.player) ((uint8_t*)out.player)[c.env] = (uint8_t)p;
-        if (out.reward) {
-            float r[G::P];
-#pragma unroll
-            for (int k = 0; k < G::P; k++) r[k] = 0.f;
-            emit_reward<G>((float*)out.reward, c.env, r);
-        }
-        if (out.done) ((uint8_t*)out.done)[c.env] = (uint8_t)g.is_over();
-        g.store(st, n, c.env);
-        ctl[c.env] = m.ctl_word();
-    }
-}
-
-template <class G>
-__global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
-                                                 const int32_t* actions, cs_step_out out, int flags,
-                                                 GameParams prm)
-{
-    CS_SMEM(G);
-    const LaneCtx c = lane_ctx(n);
-    RingLane<> m = ring_lane(mt, ctl, c);
-    G g;
-    g.bind(scratch_of<G>(scr[c.wid], c.lane), prm);
-    g.blank();
-    float r[G::P];
-#pragma unroll
-    for (int k = 0; k < G::P; k++) r[k] = 0.f;
-    bool done = false;
-    if (c.valid) {
-        g.load(st, n, c.env);
-        if (g.is_over()) {
-            game_reset(g, m, st, n, c.env);
-        } else {
-            g.step(actions[c.env], m);
-            done = g.is_over();
-            if (done) g.payoffs(r);
-        }
-    }
-    refill<G>(m, c.lane, flags & 1);
-    uint32_t bits[G::NB];
-    const int p = g.current();
-    g.observe(p, bits);
-    if (out.obs) emit_obs<G>(lds[c.wid], bits, (uint8_t*)out.obs, c.wave_first, flags, c);
-    if (c.valid) {
-        if (out.legal) emit_legal<G>((uint8_t*)out.legal, c.env, g.legal());
-        if (out.player) ((uint8_t*)out.player)[c.env] = (uint8_t)p;
-        if (out.reward) emit_reward<G>((float*)out.reward, c.env, r);
-        if (out.done) ((uint8_t*)out.done)[c.env] = (uint8_t)done;
-        g.store(st, n, c.env);
-        ctl[c.env] = m.ctl_word();
-    }
-}
-
-template <class G>
-__global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n, int player, cs_step_out out,
-                                                    GameParams prm)
-{
-    CS_SMEM(G);
-    const LaneCtx c = lane_ctx(n);
-    G g;
-    g.bind(scratch_of<G>(scr[c.wid], c.lane), prm);
-    g.blank();
-    if (c.valid) g.load(st, n, c.env);
-    uint32_t bits[G::NB];
-    g.observe(player, bits);
-    if (out.obs) emit_obs<G>(lds[c.wid], bits, (uint8_t*)out.obs, c.wave_first, 0, c);
-    if (c.valid) {
-        if (out.legal) emit_legal<G>((uint8_t*)out.legal, c.env, g.legal());
-        if (out.player) ((uint8_t*)out.player)[c.env] = (uint8_t)g.current();
-        if (out.done) ((uint8_t*)out.done)[c.env] = (uint8_t)g.is_over();
-    }
-}
-
-template <class G>
-__global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n, int T,
-                                                    uint64_t seed, uint64_t t0, uint64_t env_base, cs_traj_out out,
-                                                    int flags, GameParams prm, uint32_t* sctl, uint8_t* sbuf)
-{
-    CS_SMEM_ROWS(G, G::EPW);
-    __shared__ __attribute__((aligned(16))) uint8_t stage[WAVES_PER_BLOCK][StageBytes<G>::value];
-    const LaneCtx c = lane_ctx<G::EPW>(n);
-    RingLane<G::STAGE_MODE> m = ring_lane<G::STAGE_MODE>(mt, ctl, c);
-    // MT staging needs both blocks valid at every restage, i.e. the cooperative refill (flag bit 0 off);
-    // flag bit 1 disables it (one global load per draw) for A/B runs and fallback-path tests
-    const bool staged = !(flags & 3);
-    constexpr bool persist = G::STAGE_MODE == STAGE_LDS;
-    uint8_t* rows = nullptr;
-    if constexpr (persist) {
-        // the staged rows left by the previous launch stay valid while ctl bit 17 is set (single-step kernels and
-        // seeding rewrite ctl without it)
-        rows = sbuf + c.wave_first * G::STAGE_W;
-        if (staged) {
-            if (c.valid && ((ctl[c.env] >> 17) & 1u)) {
-                const uint32_t w = sctl[c.env];
-                m.sp = w & 0xFFFFu;
-                m.sn = w >> 16;
-            }
-            stage_rows_copy<G::STAGE_W, G::STAGE_PAD>(stage[c.wid], rows, c.lane, c.nvalid, true);
-        }
-    }
-    // the deal queues of the wave's envs for the launch: in registers, or in LDS (DQW consecutive words per lane:
-    // odd stride), per the game's DQ_REGS
-    constexpr int DQ = DqOf<G>::value, DQW = DqOf<G>::words;
-    constexpr bool QREGS = DqOf<G>::regs;
-    __shared__ uint32_t dql[DQ > 0 && !QREGS ? WAVES_PER_BLOCK * G::EPW * DQW : 1];
-    using QV = std::conditional_t<QREGS, DqRegs<DQW ? DQW : 1>, DqMem>;
-    QV q{};
-    if constexpr (DQ > 0) {
-        if constexpr (!QREGS) q = DqMem{dql + (c.wid * G::EPW + (c.lane < G::EPW ? c.lane : 0)) * DQW, 1};
-        if (c.valid) {
-#pragma unroll
-            for (int w = 0; w < DQW; w++) q.set(w, st[(int64_t)(G::GW + w) * n + c.env]);
-        }
-    }
-    G g;
-    g.bind(scratch_of<G>(scr[c.wid], c.lane), prm);
-    g.blank();
-    if (c.valid) {
-        g.load(st, n, c.env);
-        if (g.is_over()) {
-            if constexpr (DQ > 0) dq_reset(g, m, q);
-            else g.reset(m);
-        }
-    }
-    refill<G>(m, c.lane, flags & 1);
-    if (staged) restage<G>(m, stage[c.wid], c.lane, c.valid);
-    uint8_t* obs = (uint8_t*)out.obs;
-    uint8_t* legal = (uint8_t*)out.legal;
-    uint8_t* player = (uint8_t*)out.player;
-    float* reward = (float*)out.reward;
-    uint8_t* done_o = (uint8_t*)out.done;
-    const uint64_t genv = env_base + (uint64_t)c.env;
-    PolicyRng pol;
-    for (int t = 0; t < T; t++) {
-
-        const int64_t rowbase = (int64_t)t * n;
-        const int p = g.current();
-        const uint64_t lg = g.legal();
-        uint32_t bits[G::NB];
-        g.observe(p, bits);
-        const uint32_t pr = pol.at(seed, genv, t0 + (uint64_t)t, t == 0);
-        const int a = G::A <= 32 ? pick_legal32((uint32_t)lg, pr) : pick_legal(lg, pr);
-#ifndef CS_PROF_NO_OBS   // profiling builds only (tools: make variant DEFS=-DCS_PROF_NO_OBS): outputs incomplete
-        emit_obs<G, G::EPW>(lds[c.wid], bits, obs, rowbase + c.wave_first, flags, c);
-#endif
-        float r[G::P];
-#pragma unroll
-        for (int k = 0; k < G::P; k++) r[k] = 0.f;
-        bool done = false;
-        if (c.valid) {
-            const int64_t row = rowbase + c.env;
-#ifndef CS_PROF_NO_SMALL
-            emit_legal<G>(legal, row, lg);
-            out_store(player + row, (uint8_t)p);
-#endif
-            if constexpr (G::ACTION_BYTES == 1) out_store((uint8_t*)out.action + row, (uint8_t)a);
-            else out_store((int16_t*)out.action + row, (int16_t)a);
-            g.step(a, m);
-            done = g.is_over();
-            if (done) {
-                g.payoffs(r);
-                if (out.final_obs) {   // Env.run's final state of every player (envs/env.py:161-164)
-#pragma unroll
-                    for (int q = 0; q < G::P; q++) {
-                        uint32_t fb[G::NB];
-                        g.observe(q, fb);
-                        write_obs_direct<G>((uint8_t*)out.final_obs + (row * G::P + q) * G::OBS, fb);
-                    }
-                }
-            }
-#ifndef CS_PROF_NO_SMALL
-            emit_reward<G>(reward, row, r);
-            out_store(done_o + row, (uint8_t)done);
-#endif
-            if constexpr (DQ == 0) {
-                if (done) g.reset(m);
-            }
-        }
-        if constexpr (DQ > 0) {
-            // a lane ending its game with an empty queue makes every lane with room draw one deal ahead, in lockstep
-            if (__ballot(c.valid && done && (q.get(0) & 7u) == 0u)) {
-                if (c.valid && (q.get(0) & 7u) < (uint32_t)DQ) dq_push(g, m, q);
-            }
-            if (c.valid && done) dq_reset(g, m, q);
-        }
-        refill<G>(m, c.lane, flags & 1);
-        if (staged) restage<G>(m, stage[c.wid], c.lane, c.valid);
-    }
-    bool keep = false;
-    if constexpr (persist) {
-        if (staged) {
-            stage_rows_copy<G::STAGE_W, G::STAGE_PAD>(stage[c.wid], rows, c.lane, c.nvalid, false);
-            keep = true;
-        }
-    }
-    if (c.valid) {
-        g.store(st, n, c.env);
-        if constexpr (DQ > 0) {
-#pragma unroll
-            for (int w = 0; w < DQW; w++) st[(int64_t)(G::GW + w) * n + c.env] = q.get(w);
-        }
-        ctl[c.env] = m.ctl_word() | ((uint32_t)keep << 17);
-        if (keep) sctl[c.env] = m.sp | (m.sn << 16);
-    }
-}
-
-// ------------------------------------------------------------------------------------------------------------------
-static inline GameParams params_of(const Buffers& b)
-{
-    return GameParams{b.num_players, b.num_decks, b.chips_for_each, b.dealer_id};
-}
-static inline dim3 grid_for(int64_t n, int epw = WAVE)
-{
-    const int64_t per = (int64_t)WAVES_PER_BLOCK * epw;
-    return dim3((unsigned)((n + per - 1) / per));
-}
-
-template <class G>
-static hipError_t seed_g(const Buffers& b, const uint32_t* keys, const int32_t* klen, int64_t first, int64_t count,
-                         hipStream_t s)
-{
-    hipLaunchKernelGGL(k_seed<G>, grid_for(count), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, keys, klen, first,
-                       count, b.serial_refill, params_of(b));
-    return hipGetLastError();
-}
-template <class G>
-static hipError_t reset_g(const Buffers& b, const cs_step_out& o, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_reset<G>, grid_for(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, o, b.serial_refill, params_of(b));
-    return hipGetLastError();
-}
-template <class G>
-static hipError_t step_g(const Buffers& b, const int32_t* a, const cs_step_out& o, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_step<G>, grid_for(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, a, o, b.serial_refill,
-                       params_of(b));
-    return hipGetLastError();
-}
-template <class G>
-static hipError_t observe_g(const Buffers& b, int32_t p, const cs_step_out& o, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_observe<G>, grid_for(b.n), dim3(BLOCK), 0, s, b.state, b.n, p, o, params_of(b));
-    return hipGetLastError();
-}
-template <class G>
-static hipError_t rollout_g(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
-                            const cs_traj_out& o, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_rollout<G>, grid_for(b.n, G::EPW), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0,
-                       env_base, o, b.serial_refill, params_of(b), b.sctl, b.sbuf);
-    return hipGetLastError();
-}
-
-template <class G>
-static void fill_info(cs_game_info* info)
-{
-    info->obs_dim = G::OBS;
-    info->num_actions = G::A;
-    info->num_players = G::P;
-    info->legal_bytes = G::LB;
-    info->action_bytes = G::ACTION_BYTES;
-    info->state_words = G::WORDS;
-    info->action_feature_dim = G::A;
-}
-
-template <class G>
-static int64_t stage_bytes_of() { return G::STAGE_MODE == STAGE_LDS ? G::STAGE_W : 0; }
-
 int64_t stage_bytes_per_env(int32_t game, int32_t num_players)
 {
     switch (game) {
-    case CS_GAME_LEDUC: return stage_bytes_of<Leduc>();
-    case CS_GAME_LIMIT: return stage_bytes_of<Limit>();
+    case CS_GAME_LEDUC: return num_players > 2 ? np_stage_bytes(game, num_players) : stage_bytes_of<Leduc>();
+    case CS_GAME_LIMIT: return num_players > 2 ? np_stage_bytes(game, num_players) : stage_bytes_of<Limit>();
     case CS_GAME_BLACKJACK: return num_players <= 1 ? stage_bytes_of<Blackjack<1>>() : stage_bytes_of<Blackjack<4>>();
-    case CS_GAME_NOLIMIT: return stage_bytes_of<Nolimit>();
+    case CS_GAME_NOLIMIT: return num_players > 2 ? np_stage_bytes(game, num_players) : stage_bytes_of<Nolimit>();
     default: return 0;
     }
 }
@@ -639,10 +26,12 @@ int game_info(int32_t game, const cs_config* cfg, cs_game_info* info)
 {
     switch (game) {
     case CS_GAME_LEDUC:
+        if (cfg && cfg->num_players > 2) return np_game_info(game, cfg->num_players, info);
         if (cfg && cfg->num_players != 0 && cfg->num_players != 2) return CS_E_UNSUPPORTED;
         fill_info<Leduc>(info);
         return CS_OK;
     case CS_GAME_LIMIT:
+        if (cfg && cfg->num_players > 2) return np_game_info(game, cfg->num_players, info);
         if (cfg && cfg->num_players != 0 && cfg->num_players != 2) return CS_E_UNSUPPORTED;
         fill_info<Limit>(info);
         return CS_OK;
@@ -656,13 +45,16 @@ int game_info(int32_t game, const cs_config* cfg, cs_game_info* info)
         else fill_info<Blackjack<4>>(info);
         return CS_OK;
     }
-    case CS_GAME_NOLIMIT:
-        if (cfg && cfg->num_players != 0 && cfg->num_players != 2) return CS_E_UNSUPPORTED;
+    case CS_GAME_NOLIMIT: {
+        const int np = (cfg && cfg->num_players > 0) ? cfg->num_players : 2;
         if (cfg && (cfg->chips_for_each < 0 || cfg->chips_for_each > 255 || cfg->dealer_plus1 < 0 ||
-                    cfg->dealer_plus1 > 2))
+                    cfg->dealer_plus1 > np))
             return CS_E_UNSUPPORTED;
+        if (np > 2) return np_game_info(game, np, info);
+        if (np != 2) return CS_E_UNSUPPORTED;
         fill_info<Nolimit>(info);
         return CS_OK;
+    }
     case CS_GAME_DOUDIZHU:
         if (cfg && cfg->num_players != 0 && cfg->num_players != ddz::P) return CS_E_UNSUPPORTED;
         info->obs_dim = ddz::OBS;
@@ -716,6 +108,7 @@ hipError_t launch_seed(const Buffers& b, const uint32_t* keys, const int32_t* kl
 {
 #define C_(G) seed_g<G>(b, keys, klen, first, count, s)
     if (b.game == CS_GAME_DOUDIZHU) return C_(ddz::SeedView);
+    if (is_holdem_n(b)) return np_launch_seed(b, keys, klen, first, count, s);
     CS_DISPATCH(b.game, C_)
 #undef C_
 }
@@ -723,6 +116,7 @@ hipError_t launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s)
 {
 #define C_(G) reset_g<G>(b, o, s)
     if (b.game == CS_GAME_DOUDIZHU) return ddz::launch_reset(b, o, s);
+    if (is_holdem_n(b)) return np_launch_reset(b, o, s);
     CS_DISPATCH(b.game, C_)
 #undef C_
 }
@@ -730,6 +124,7 @@ hipError_t launch_step(const Buffers& b, const int32_t* a, const cs_step_out& o,
 {
 #define C_(G) step_g<G>(b, a, o, s)
     if (b.game == CS_GAME_DOUDIZHU) return ddz::launch_step(b, a, o, s);
+    if (is_holdem_n(b)) return np_launch_step(b, a, o, s);
     CS_DISPATCH(b.game, C_)
 #undef C_
 }
@@ -737,6 +132,7 @@ hipError_t launch_observe(const Buffers& b, int32_t p, const cs_step_out& o, hip
 {
 #define C_(G) observe_g<G>(b, p, o, s)
     if (b.game == CS_GAME_DOUDIZHU) return ddz::launch_observe(b, p, o, s);
+    if (is_holdem_n(b)) return np_launch_observe(b, p, o, s);
     CS_DISPATCH(b.game, C_)
 #undef C_
 }
@@ -745,6 +141,7 @@ hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t
 {
 #define C_(G) rollout_g<G>(b, T, seed, t0, env_base, o, s)
     if (b.game == CS_GAME_DOUDIZHU) return ddz::launch_rollout(b, T, seed, t0, env_base, o, s);
+    if (is_holdem_n(b)) return np_launch_rollout(b, T, seed, t0, env_base, o, s);
     CS_DISPATCH(b.game, C_)
 #undef C_
 }

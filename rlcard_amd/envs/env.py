@@ -178,7 +178,7 @@ class Env(object):
         if not self._history:
             return False
         words, last, payoffs = self._history.pop()
-        gw = self._vec.GAME_WORDS.get(self._vec.env_id)
+        gw = self._vec.game_words
         if gw is not None:   # hold'em: the game words only; deals already drawn ahead stay queued
             words = list(words[:gw]) + self._vec.env_state_words(0)[gw:]
         self._vec.set_env_state_words(0, words)

@@ -25,7 +25,12 @@ class LeducholdemEnv(Env):
         return self.actions[action_id]
 
     def _fields(self):
-        w0, w1 = self._state_words()
+        w = self._state_words()
+        if self.num_players > 2:   # cs_holdem_n.h LeducN: a word per player (hand:3 in:5), then pub:3 rc:2 ptr:3
+            P, sw = self.num_players, w[self.num_players]
+            return dict(h=[x & 7 for x in w[:P]], pub=sw & 7, chips=[(x >> 3) & 31 for x in w[:P]],
+                        rc=(sw >> 3) & 3, ptr=(sw >> 5) & 7)
+        w0, w1 = w[:2]
         return dict(h=[w0 & 7, (w0 >> 3) & 7], pub=(w0 >> 6) & 7, chips=[(w0 >> 9) & 31, (w0 >> 14) & 31],
                     rc=w1 & 3, ptr=(w1 >> 2) & 1)
 

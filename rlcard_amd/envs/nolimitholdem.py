@@ -49,11 +49,20 @@ class NolimitholdemEnv(Env):
         return raw.value if isinstance(raw, Action) else int(raw)
 
     def _fields(self):
+        stack = int(self.game_config['chips_for_each'])
+        if self.num_players > 2:   # cs_holdem_n.h NolimitN: a word per player (c0 c1 in:8@12), board, ptr/rc
+            w = self._state_words()
+            P = self.num_players
+            b, s1 = w[P], w[P + 1]
+            rc = (s1 >> 4) & 7
+            nboard = 0 if rc == 0 else min(5, rc + 2)
+            chips = [(x >> 12) & 255 for x in w[:P]]
+            return dict(hands=[[x & 63, (x >> 6) & 63] for x in w[:P]], board=[(b >> (6 * k)) & 63 for k in range(nboard)],
+                        chips=chips, stakes=[stack - c for c in chips], ptr=s1 & 15, rc=rc)
         w0, w1, w2, w3 = self._state_words()[:4]
         rc = (w0 >> 27) & 7
         nboard = 0 if rc == 0 else min(5, rc + 2)
         chips = [w2 & 255, (w2 >> 8) & 255]
-        stack = int(self.game_config['chips_for_each'])
         return dict(hands=[[w0 & 63, (w0 >> 6) & 63], [(w0 >> 12) & 63, (w0 >> 18) & 63]],
                     board=[(w1 >> (6 * k)) & 63 for k in range(nboard)], chips=chips,
                     stakes=[stack - c for c in chips], ptr=(w0 >> 24) & 1, rc=rc)

@@ -212,12 +212,19 @@ class VecEnv:
         (rlcard_amd/csrc/cs_ring.h), doudizhu's word layout 2."""
         return 1248 if self.env_id == 'doudizhu' else 2496
 
-    # hold'em games keep a deal queue after their 4 game words (rlcard_amd/csrc/cs_limit.h): deals drawn ahead
+    # heads-up hold'em games keep a deal queue after their 4 game words (rlcard_amd/csrc/cs_limit.h): deals drawn
+    # ahead. 3..6-player hold'em has none (its judge may draw from the stream at a game's end, cs_holdem_n.h).
     GAME_WORDS = {'limit-holdem': 4, 'no-limit-holdem': 4}
+
+    @property
+    def game_words(self):
+        """Packed game words before the deal queue, None when the game has no queue."""
+        return self.GAME_WORDS.get(self.env_id) if self.num_players == 2 else None
 
     def game_state_words(self, env):
         """The packed game words of env `env` (without the hold'em deal queue)."""
-        return self.env_state_words(env)[:self.GAME_WORDS.get(self.env_id, self.info.state_words)]
+        gw = self.game_words
+        return self.env_state_words(env)[:gw if gw is not None else self.info.state_words]
 
     def rng_position(self, env):
         """Draws consumed by env `env`, modulo rng_period. Deals already drawn into a hold'em env's deal queue
@@ -225,7 +232,7 @@ class VecEnv:
         v = C.c_uint32()
         _abi.check(_abi.lib().cs_get_rng_ctl(self._h, int(env), C.byref(v)), 'cs_get_rng_ctl')
         pos = v.value & (0x7FF if self.env_id == 'doudizhu' else 0xFFF)
-        gw = self.GAME_WORDS.get(self.env_id)
+        gw = self.game_words
         if gw is not None and self.info.state_words > gw:
             w = self.env_state_words(env)
             cap = (len(w) - gw - 1) // 2

@@ -60,3 +60,18 @@ def test_invalid_arguments_are_rejected():
     info = _abi.GameInfo()
     assert _abi.lib().cs_game_info_get(9, None, C.byref(info)) == -4
     assert _abi.lib().cs_create(None, 1, 64, 0, None) == -1
+
+
+def test_nplayer_game_info():
+    """game_num_players 3..6 (Leduc 3..5): same obs / action shapes, one packed word per player plus shared words,
+    no deal queue (cs_holdem_n.h); counts past the engine's range are refused."""
+    for game, words_extra, top in (('leduc-holdem', 1, 5), ('limit-holdem', 3, 6), ('no-limit-holdem', 2, 6)):
+        two, _ = _abi.game_info(game, 2)
+        for n in range(3, top + 1):
+            info, _ = _abi.game_info(game, n)
+            assert (info.obs_dim, info.num_actions, info.legal_bytes) == (two.obs_dim, two.num_actions, two.legal_bytes)
+            assert info.num_players == n and info.state_words == n + words_extra
+        with pytest.raises(_abi.CardsimError):
+            _abi.game_info(game, top + 1)
+    info, _ = _abi.game_info('no-limit-holdem', 6, chips_for_each=50, dealer_id=5)
+    assert info.num_players == 6

@@ -1,0 +1,130 @@
+"""3..6-player hold'em ('game_num_players') on the HIP engine vs the reference streams and the CPU oracle, through the
+C ABI. Needs a GPU. Kernels: rlcard_amd/csrc/cs_holdem_n.h; oracle: oracle/or_leduc.c, or_limit.c, or_nolimit.c,
+or_judger.c; fixtures: tests/golden/*_np.npz (tests/golden/gen_golden.py --only nplayer)."""
+import numpy as np
+import pytest
+
+import golden_replay as gr
+from rlcard_amd import seeding
+
+torch = pytest.importorskip('torch')
+pytestmark = pytest.mark.gpu
+
+FIXTURES = [('leduc-holdem', 'leduc_np'), ('limit-holdem', 'limit_np'), ('no-limit-holdem', 'nolimit_np')]
+CASES = [('leduc-holdem', 3, {}), ('leduc-holdem', 5, {}), ('limit-holdem', 3, {}), ('limit-holdem', 6, {}),
+         ('no-limit-holdem', 4, {}), ('no-limit-holdem', 6, {'chips_for_each': 10}),
+         ('no-limit-holdem', 3, {'chips_for_each': 6, 'dealer_id': 2})]
+
+
+def _np(o):
+    return {k: v.cpu().numpy() for k, v in o.items()}
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail('GPU tests need a visible GPU (run them on the MI355X box)')
+
+
+def _vec(game, n, **kw):
+    from rlcard_amd import VecEnv
+    return VecEnv(game, n, **kw)
+
+
+def _oracle(oracle, game, seeds, np_, cfg):
+    keys, lens = seeding.seed_keys(seeds)
+    d = cfg.get('dealer_id')
+    return oracle.Batch(game, len(seeds), keys, lens, num_players=np_, chips_for_each=cfg.get('chips_for_each', 100),
+                        dealer_id=-1 if d is None else d)
+
+
+def _same(got, exp, what):
+    for k in exp:
+        if k not in got:
+            continue
+        g, e = got[k], exp[k].astype(got[k].dtype)
+        if not np.array_equal(g, e):
+            bad = np.argwhere(g != e)
+            raise AssertionError('%s: %s differs at %d places, first %s: got %s expected %s'
+                                 % (what, k, len(bad), bad[0], g[tuple(bad[0])], e[tuple(bad[0])]))
+
+
+@pytest.mark.parametrize('game,name', FIXTURES)
+def test_single_env_replays_reference_nplayer_stream(game, name):
+    d = gr.load(name)
+
+    class One:
+        def __init__(self, ei, seed):
+            self.v = _vec(game, 1, seeds=[seed], config=gr.env_config(d, ei))
+
+        def reset(self):
+            return {k: x[0] for k, x in _np(self.v.reset()).items()}
+
+        def step(self, a):
+            return {k: x[0] for k, x in _np(self.v.step([a])).items()}
+
+        def observe(self, p):
+            o = _np(self.v.observe(p))
+            return o['obs'][0], o['legal'][0]
+
+    assert gr.replay(d, One, 5 if game == 'no-limit-holdem' else 4) == len(d['ev_kind'])
+
+
+@pytest.mark.parametrize('game,players,cfg', CASES)
+def test_nplayer_step_api_matches_oracle(oracle, game, players, cfg):
+    n, steps = 3000, 100
+    v = _vec(game, n, seed=100, config=dict(cfg, game_num_players=players))
+    assert v.num_players == players
+    ob = _oracle(oracle, game, list(range(100, 100 + n)), players, cfg)
+    rng = np.random.RandomState(1)
+    _same(_np(v.reset()), ob.reset(), 'reset')
+    for t in range(steps):
+        acts = rng.randint(-1, v.num_actions + 1, size=n).astype(np.int32)   # includes illegal ids
+        _same(_np(v.step(torch.from_numpy(acts).cuda())), ob.step(acts), 'step %d' % t)
+    for p in range(players):
+        o = _np(v.observe(p))
+        for i in (0, 1, n // 2, n - 1):
+            obs, legal = ob.observe(i, p)
+            assert np.array_equal(o['obs'][i], obs) and np.array_equal(o['legal'][i], legal), (p, i)
+
+
+@pytest.mark.parametrize('flags', [0, 1])   # 1: serial MT refill in-lane
+@pytest.mark.parametrize('game,players,cfg', CASES)
+def test_nplayer_rollout_matches_oracle(oracle, game, players, cfg, flags):
+    """Three chained launches of 64 steps (Limit / No-limit cross several MT ring refills), then the stream
+    positions; final observations of every player where a game ends."""
+    n, T = 2000 + 37, 64
+    v = _vec(game, n, seed=7, config=dict(cfg, game_num_players=players))
+    v.set_kernel_flags(flags)
+    ob = _oracle(oracle, game, list(range(7, 7 + n)), players, cfg)
+    v.reset()
+    ob.reset()
+    for chunk in range(3):
+        got = _np(v.rollout(T, policy_seed=99, t0=chunk * T, final_obs=True))
+        exp = ob.rollout(T, 99, chunk * T, 0, final_obs=True)
+        done = exp['done'].astype(bool)
+        got['final_obs'] = got['final_obs'][done]
+        exp['final_obs'] = exp['final_obs'][done]
+        _same(got, exp, 'rollout chunk %d' % chunk)
+        r = got['reward'][done]
+        assert np.all(np.abs(r.sum(-1)) < 1e-4), 'zero-sum payoffs'
+    torch.cuda.synchronize()
+    for i in (0, 63, 64, n // 2, n - 1):
+        assert v.rng_position(i) == ob.draws(i) % v.rng_period
+
+
+@pytest.mark.parametrize('game,players', [('leduc-holdem', 4), ('limit-holdem', 5), ('no-limit-holdem', 6)])
+def test_nplayer_compat_env(game, players):
+    """rlcard_amd.make with game_num_players: shapes, raw_obs decoding of the N-player state words, Env.run."""
+    import rlcard_amd
+    from rlcard_amd.agents import RandomAgent
+    env = rlcard_amd.make(game, config={'seed': 3, 'game_num_players': players})
+    assert env.num_players == players and len(env.state_shape) == players
+    env.set_agents([RandomAgent(num_actions=env.num_actions) for _ in range(players)])
+    for _ in range(5):
+        traj, payoffs = env.run(is_training=False)
+        assert len(traj) == players and len(payoffs) == players
+        assert abs(float(np.sum(payoffs))) < 1e-6
+        for p in range(players):
+            raw = traj[p][-1]['raw_obs']
+            assert len(raw['all_chips']) == players
