@@ -161,6 +161,54 @@ int cs_action_features(cs_handle* h, const int32_t* ids, int64_t count, void* fe
 int cs_cfr_train(cs_handle* h, int32_t iterations, int64_t iteration0, double* policy, double* average_policy,
                  double* regrets, uint32_t* flags, void* stream);
 
+/* ---- DMC learner side (rlcard/agents/dmc_agent/) ----------------------------------------------------------------
+ * Actor buffers (utils.py:97-163 act): every (env, player) of a handle keeps its stream of transitions -- state = the
+ * obs the player acted on (int8 [obs_dim]), action = Env.get_action_feature of its action (int8 [action_feature_dim]),
+ * target = the player's payoff of that game on each of its rows, done / episode_return set on its last row of the
+ * game -- and a T-row chunk is handed out once more than T rows of finished games are queued (`while size[p] > T`).
+ * The streams live in a ring of `slots` chunks per (env, player) in HBM. Chunk ids handed out by cs_dmc_fill must be
+ * gathered (cs_dmc_gather) before the next cs_dmc_fill reuses their slots; rows that would overwrite a chunk still
+ * held are dropped and flagged (cs_dmc_status). Needs slots * T >= T + the rows one fill adds per (env, player) +
+ * the longest game's rows. */
+typedef struct cs_dmc cs_dmc;
+
+/* get_batch (utils.py:33-46) output, DEVICE pointers, [T][B] rows (any may be NULL):
+ *   state int8 [T][B][state_dim(player)] (doudizhu landlord 790, peasants 901), action int8 [T][B][feature_dim],
+ *   target float [T][B], done uint8 [T][B], episode_return float [T][B] */
+typedef struct {
+    void* state;
+    void* action;
+    void* target;
+    void* done;
+    void* episode_return;
+} cs_dmc_batch;
+
+int cs_dmc_create(cs_handle* h, int32_t T, int32_t slots, cs_dmc** out);
+void cs_dmc_destroy(cs_dmc* d);
+/* Append the rows of a trajectory of this handle (cs_rollout layout [T_roll][n]; needs obs, player, action, reward,
+ * done; player >= num_players marks a row that is not a transition) to the streams, in time order. The chunks that
+ * become ready are listed in ready (int64 [cap], DEVICE) as ids, in (env, player, chunk) order; *nready (int64,
+ * DEVICE) = their number (entries past cap are not written). Replaces the per-actor act loop for every env at once. */
+int cs_dmc_fill(cs_dmc* d, int32_t T_roll, const cs_traj_out* traj, int64_t* ready, int64_t cap, int64_t* nready,
+                void* stream);
+/* get_batch: `count` chunk ids (DEVICE int64, all of player `player`) stacked along dim 1 into `out`. */
+int cs_dmc_gather(cs_dmc* d, int32_t player, const int64_t* chunks, int64_t count, const cs_dmc_batch* out,
+                  void* stream);
+/* Synchronous: bit 0 = rows were dropped because a stream's ring was full (slots too few, or chunks not gathered). */
+int cs_dmc_status(cs_dmc* d, uint32_t* host_flags);
+
+/* DMCNet scoring of legal actions (model.py:21-43 forward, 91-110 predict), first layer fused: for entry i (state
+ * state_of[i], action ids[i]) h1[i] = relu(X[state_of[i]] + b1 + W_act . feature(ids[i])), X = W_obs . obs precomputed
+ * per state ([S][H] float), W_act float [feature_dim][H] (the first Linear's action columns, transposed), b1 [H],
+ * h1 float [E][H]; H a multiple of 4. Features as cs_action_features. All DEVICE memory. */
+int cs_dmc_layer1(cs_handle* h, const float* X, const int32_t* state_of, const int32_t* ids, int64_t E, int32_t H,
+                  const float* W_act, const float* b1, float* h1, void* stream);
+/* Per state s (legal entries [offsets[s], offsets[s] + counts[s]) of values / ids, cs_legal_lists layout): the id with
+ * the largest value (np.argmax: first maximum), or with probability eps a uniform legal id (DMCAgent.step; Philox
+ * keyed by seed on (state_base + s, t) in place of np.random). actions int32 [S], -1 where a state has no entry. */
+int cs_dmc_select(const float* values, const int32_t* counts, const int64_t* offsets, const int32_t* ids, int64_t S,
+                  float eps, uint64_t seed, uint64_t t, uint64_t state_base, int32_t* actions, void* stream);
+
 /* Copy the packed state words of env `env` (state_words u32, HOST buffer) -- the raw fields behind
  * Env.get_state()['raw_obs'] / get_perfect_information for single-env compatibility and debugging. Limit and
  * No-limit hold'em: 4 game words, then the env's deal queue (deals the rollout drew ahead from the stream; a header

@@ -40,12 +40,18 @@ class TransOut(C.Structure):
                 ('ret', C.c_void_p)]
 
 
+class DmcBatch(C.Structure):
+    _fields_ = [('state', C.c_void_p), ('action', C.c_void_p), ('target', C.c_void_p), ('done', C.c_void_p),
+                ('episode_return', C.c_void_p)]
+
+
 # every symbol include/cardsim.h declares (tests check the library exports all of them)
 SYMBOLS = ('cs_game_info_get', 'cs_create', 'cs_destroy', 'cs_seed', 'cs_reset', 'cs_step', 'cs_observe',
            'cs_rollout', 'cs_transitions', 'cs_legal_lists', 'cs_action_features', 'cs_get_env_state',
            'cs_set_env_state', 'cs_copy_env_state', 'cs_get_rng_ctl', 'cs_cfr_train', 'cs_debug_holdem_rank7', 'cs_debug_ddz_legal',
            'cs_debug_set_serial_refill', 'cs_debug_set_kernel_flags',
-           'cs_last_error', 'cs_version')
+           'cs_dmc_create', 'cs_dmc_destroy', 'cs_dmc_fill', 'cs_dmc_gather', 'cs_dmc_status', 'cs_dmc_layer1',
+           'cs_dmc_select', 'cs_last_error', 'cs_version')
 
 _lib = None
 
@@ -84,10 +90,18 @@ def lib():
     L.cs_debug_ddz_legal.argtypes = [vp, vp, vp, i64, vp, vp]
     L.cs_debug_set_serial_refill.argtypes = [vp, i32]
     L.cs_debug_set_kernel_flags.argtypes = [vp, i32]
+    L.cs_dmc_create.argtypes = [vp, i32, i32, C.POINTER(vp)]
+    L.cs_dmc_destroy.argtypes = [vp]
+    L.cs_dmc_destroy.restype = None
+    L.cs_dmc_fill.argtypes = [vp, i32, C.POINTER(TrajOut), vp, i64, vp, vp]
+    L.cs_dmc_gather.argtypes = [vp, i32, vp, i64, C.POINTER(DmcBatch), vp]
+    L.cs_dmc_status.argtypes = [vp, vp]
+    L.cs_dmc_layer1.argtypes = [vp, vp, vp, vp, i64, i32, vp, vp, vp, vp]
+    L.cs_dmc_select.argtypes = [vp, vp, vp, vp, i64, C.c_float, u64, u64, u64, vp, vp]
     L.cs_last_error.restype = C.c_char_p
     L.cs_version.restype = C.c_char_p
     for name in SYMBOLS:
-        if name not in ('cs_destroy', 'cs_last_error', 'cs_version'):
+        if name not in ('cs_destroy', 'cs_dmc_destroy', 'cs_last_error', 'cs_version'):
             getattr(L, name).restype = C.c_int
     _lib = L
     return L

@@ -81,6 +81,9 @@ int cs_create(cs_handle** out, int32_t game, int64_t num_envs, int32_t device, c
     h->b.game = game;
     h->b.n = num_envs;
     h->b.num_players = info.num_players;
+    h->b.obs_dim = info.obs_dim;
+    h->b.num_actions = info.num_actions;
+    h->b.action_bytes = info.action_bytes;
     h->b.num_decks = cfg ? cfg->num_decks : 1;
     h->b.chips_for_each = (cfg && cfg->chips_for_each > 0) ? cfg->chips_for_each : 100;
     h->b.dealer_id = cfg ? cfg->dealer_plus1 - 1 : -1;
@@ -217,6 +220,129 @@ int cs_rollout(cs_handle* h, int32_t T, uint64_t policy_seed, uint64_t t0, uint6
     if (r != CS_OK) return r;
     hipError_t e = cs::launch_rollout(h->b, T, policy_seed, t0, env_base, *out, (hipStream_t)stream);
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_rollout");
+}
+
+// ---- DMC ----------------------------------------------------------------------------------------------------------
+struct cs_dmc {
+    cs_handle* h;
+    cs::DmcRing r;
+    void* mem;          // one allocation for the ring and the counters
+    int64_t* dst;       // [rows] ring row of each trajectory row (grown on demand)
+    int64_t dst_rows;
+    void* scan_tmp;
+    size_t scan_bytes;
+};
+
+int cs_dmc_create(cs_handle* h, int32_t T, int32_t slots, cs_dmc** out)
+{
+    if (!h || !out) return fail(CS_E_INVALID, "null argument");
+    *out = nullptr;
+    if (T <= 0 || slots < 2) return fail(CS_E_INVALID, "cs_dmc_create: T > 0 and slots >= 2");
+    int r = set_device(h);
+    if (r != CS_OK) return r;
+    const int64_t streams = h->b.n * h->info.num_players, rows = streams * slots * (int64_t)T;
+    const int64_t O = h->info.obs_dim, F = h->info.action_feature_dim;
+    auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
+    const int64_t o_st = 0, o_act = o_st + al(rows * O), o_tgt = o_act + al(rows * F), o_ret = o_tgt + al(rows * 4),
+                  o_dne = o_ret + al(rows * 4), o_ctr = o_dne + al(rows), o_gs = o_ctr + al(streams * 8),
+                  o_em = o_gs + al(streams * 8), o_cnt = o_em + al(streams * 8), o_off = o_cnt + al((streams + 1) * 4),
+                  o_flag = o_off + al((streams + 1) * 8), total = o_flag + 256;
+    cs_dmc* d = new (std::nothrow) cs_dmc();
+    if (!d) return fail(CS_E_INVALID, "out of host memory");
+    hipError_t e = hipMalloc(&d->mem, (size_t)total);
+    if (e != hipSuccess) { delete d; return fail_hip(e, "cs_dmc_create"); }
+    uint8_t* m = (uint8_t*)d->mem;
+    // counters, counts (incl. the trailing 0) and the flag start at zero; the ring rows are written before read
+    e = hipMemset(m + o_ctr, 0, (size_t)(total - o_ctr));
+    if (e != hipSuccess) { (void)hipFree(d->mem); delete d; return fail_hip(e, "cs_dmc_create"); }
+    d->h = h;
+    d->r = cs::DmcRing{T, slots, (int32_t)F, (int8_t*)(m + o_st), (int8_t*)(m + o_act), (float*)(m + o_tgt),
+                       (float*)(m + o_ret), m + o_dne, (int64_t*)(m + o_ctr), (int64_t*)(m + o_gs),
+                       (int64_t*)(m + o_em), (int32_t*)(m + o_cnt), (int64_t*)(m + o_off), (uint32_t*)(m + o_flag)};
+    d->dst = nullptr;
+    d->dst_rows = 0;
+    d->scan_tmp = nullptr;
+    d->scan_bytes = 0;
+    *out = d;
+    return CS_OK;
+}
+
+void cs_dmc_destroy(cs_dmc* d)
+{
+    if (!d) return;
+    (void)hipSetDevice(d->h->device);
+    if (d->mem) (void)hipFree(d->mem);
+    if (d->dst) (void)hipFree(d->dst);
+    if (d->scan_tmp) (void)hipFree(d->scan_tmp);
+    delete d;
+}
+
+int cs_dmc_fill(cs_dmc* d, int32_t T_roll, const cs_traj_out* traj, int64_t* ready, int64_t cap, int64_t* nready,
+                void* stream)
+{
+    if (!d || !traj || !nready || (cap > 0 && !ready)) return fail(CS_E_INVALID, "null argument");
+    if (!traj->player || !traj->done || !traj->reward) return fail(CS_E_INVALID, "traj needs player, reward and done");
+    if (T_roll <= 0) return fail(CS_E_INVALID, "T_roll must be positive");
+    int r = set_device(d->h);
+    if (r != CS_OK) return r;
+    const int64_t rows = (int64_t)T_roll * d->h->b.n;
+    if (rows > d->dst_rows) {
+        if (d->dst) (void)hipFree(d->dst);
+        d->dst = nullptr;
+        d->dst_rows = 0;
+        hipError_t e = hipMalloc((void**)&d->dst, (size_t)rows * sizeof(int64_t));
+        if (e != hipSuccess) return fail_hip(e, "cs_dmc_fill");
+        d->dst_rows = rows;
+    }
+    hipError_t e = cs::launch_dmc_fill(d->h->b, d->r, T_roll, *traj, ready, cap, nready, d->dst, &d->scan_tmp,
+                                       &d->scan_bytes, (hipStream_t)stream);
+    return e == hipSuccess ? CS_OK : fail_hip(e, "cs_dmc_fill");
+}
+
+int cs_dmc_gather(cs_dmc* d, int32_t player, const int64_t* chunks, int64_t count, const cs_dmc_batch* out,
+                  void* stream)
+{
+    if (!d || !out || (count > 0 && !chunks)) return fail(CS_E_INVALID, "null argument");
+    if (player < 0 || player >= d->h->info.num_players) return fail(CS_E_INVALID, "player out of range");
+    if (count < 0 || count > 0x7FFFFFFF) return fail(CS_E_INVALID, "count out of range");
+    if (count == 0) return CS_OK;
+    int r = set_device(d->h);
+    if (r != CS_OK) return r;
+    const int32_t sd = d->h->b.game == CS_GAME_DOUDIZHU && player == 0 ? cs::ddz::OBS_LANDLORD : d->h->info.obs_dim;
+    hipError_t e = cs::launch_dmc_gather(d->r, sd, d->h->info.obs_dim, chunks, count, *out, (hipStream_t)stream);
+    return e == hipSuccess ? CS_OK : fail_hip(e, "cs_dmc_gather");
+}
+
+int cs_dmc_status(cs_dmc* d, uint32_t* host_flags)
+{
+    if (!d || !host_flags) return fail(CS_E_INVALID, "null argument");
+    int r = set_device(d->h);
+    if (r != CS_OK) return r;
+    hipError_t e = hipMemcpy(host_flags, d->r.flag, sizeof(uint32_t), hipMemcpyDeviceToHost);
+    return e == hipSuccess ? CS_OK : fail_hip(e, "cs_dmc_status");
+}
+
+int cs_dmc_layer1(cs_handle* h, const float* X, const int32_t* state_of, const int32_t* ids, int64_t E, int32_t H,
+                  const float* W_act, const float* b1, float* h1, void* stream)
+{
+    if (!h || !X || !state_of || !ids || !W_act || !b1 || !h1) return fail(CS_E_INVALID, "null argument");
+    if (E < 0 || E > 0x7FFFFFFF || H <= 0 || H % 4) return fail(CS_E_INVALID, "E / H out of range");
+    if (E == 0) return CS_OK;
+    int r = set_device(h);
+    if (r != CS_OK) return r;
+    hipError_t e = cs::launch_dmc_layer1(X, state_of, ids, E, H, W_act, b1, h->info.action_feature_dim, h->b, h1,
+                                         (hipStream_t)stream);
+    return e == hipSuccess ? CS_OK : fail_hip(e, "cs_dmc_layer1");
+}
+
+int cs_dmc_select(const float* values, const int32_t* counts, const int64_t* offsets, const int32_t* ids, int64_t S,
+                  float eps, uint64_t seed, uint64_t t, uint64_t state_base, int32_t* actions, void* stream)
+{
+    if (!values || !counts || !offsets || !ids || !actions) return fail(CS_E_INVALID, "null argument");
+    if (S <= 0) return fail(CS_E_INVALID, "S must be positive");
+    hipError_t e = cs::launch_dmc_select(values, counts, offsets, ids, S, eps, seed, t, state_base, actions,
+                                         (hipStream_t)stream);
+    return e == hipSuccess ? CS_OK : fail_hip(e, "cs_dmc_select");
 }
 
 int cs_transitions(cs_handle* h, int32_t T, const cs_traj_out* traj, const cs_trans_out* out, void* stream)

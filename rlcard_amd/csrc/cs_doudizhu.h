@@ -76,5 +76,16 @@ struct SeedView {
     }
 };
 
+#ifdef __HIPCC__
+// _cards2array (envs/doudizhu.py:150-166) of packed counts: bit 4r + k = (count_r > k) for r < 13, bit 52 / 53 = jokers
+__device__ __forceinline__ uint64_t cards_bits(uint64_t c)
+{
+    const uint64_t lo = c & 0x000FFFFFFFFFFFFFull, H = 0x0008888888888888ull;
+    const uint64_t t = (((lo + 0x0007777777777777ull) & H) >> 3) | (((lo + 0x0006666666666666ull) & H) >> 2) |
+                       (((lo + 0x0005555555555555ull) & H) >> 1) | ((lo + 0x0004444444444444ull) & H);
+    return t | ((uint64_t)(((c >> 52) & 15u) != 0) << 52) | ((uint64_t)(((c >> 56) & 15u) != 0) << 53);
+}
+#endif
+
 }  // namespace ddz
 }  // namespace cs

@@ -20,6 +20,23 @@ struct Buffers {
     int32_t num_players, num_decks;
     int32_t chips_for_each, dealer_id;   // no-limit hold'em (cs_config; dealer_id -1 = drawn)
     int32_t serial_refill;  // testing hook
+    int32_t obs_dim, num_actions, action_bytes;   // cs_game_info of the handle
+};
+
+// DMC actor-buffer ring of a handle (cs_dmc.hip): per (env, player) stream, `slots` chunks of T rows
+struct DmcRing {
+    int32_t T, slots, F;          // rows per chunk, chunks per stream, action feature bytes
+    int8_t* st;                   // [streams][slots][T][obs_dim]
+    int8_t* act;                  // [streams][slots][T][F]
+    float* tgt;                   // [streams][slots][T]
+    float* ret;
+    uint8_t* dne;
+    int64_t* ctr;                 // [streams] rows appended
+    int64_t* gstart;              // [streams] first row of the game in progress
+    int64_t* emitted;             // [streams] chunks handed out
+    int32_t* counts;              // [streams + 1] chunks ready in the last fill (last entry 0)
+    int64_t* offsets;             // [streams + 1]
+    uint32_t* flag;               // bit 0: rows dropped (ring full)
 };
 
 int game_info(int32_t game, const cs_config* cfg, cs_game_info* info);
@@ -49,6 +66,17 @@ inline bool is_holdem_n(const Buffers& b)
 {
     return (b.game == CS_GAME_LEDUC || b.game == CS_GAME_LIMIT || b.game == CS_GAME_NOLIMIT) && b.num_players > 2;
 }
+
+// cs_dmc.hip
+hipError_t launch_dmc_fill(const Buffers& b, const DmcRing& d, int32_t T, const cs_traj_out& tr, int64_t* ready,
+                           int64_t cap, int64_t* nready, int64_t* dst, void** tmp, size_t* tmp_bytes, hipStream_t s);
+hipError_t launch_dmc_gather(const DmcRing& d, int32_t state_dim, int32_t obs_dim, const int64_t* chunks,
+                             int64_t count, const cs_dmc_batch& o, hipStream_t s);
+hipError_t launch_dmc_layer1(const float* X, const int32_t* state_of, const int32_t* ids, int64_t E, int32_t H,
+                             const float* Wa, const float* b1, int32_t F, const Buffers& b, float* h1, hipStream_t s);
+hipError_t launch_dmc_select(const float* values, const int32_t* counts, const int64_t* offsets, const int32_t* ids,
+                             int64_t S, float eps, uint64_t seed, uint64_t t, uint64_t base, int32_t* actions,
+                             hipStream_t s);
 
 // cs_cfr.hip: chance-sampling CFR tables on Leduc (device pointers, [CFR_NI][4] fp64 + [CFR_NI] u32 flags)
 constexpr int CFR_NI = 2700;
