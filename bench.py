@@ -9,6 +9,10 @@ independent, so the timed loop has no data-path collective (weak scaling, `value
 one real exchange, returning the trajectory shards to one place (--gather rank0, the default: point-to-point RCCL
 into rank 0 over xGMI; --gather all: all-gather into every rank), reported under "gather".
 
+A third phase times the same workload with the engine's fast RNG mode (cs_config.rng_mode = CS_RNG_PHILOX: Philox
+byte stream instead of numpy's MT19937, so NOT the reference's deals) and reports it under "rng_philox" -- `value`
+is always the reference-compatible MT19937 stream.
+
   python bench.py [--gpus N] [--steps K] [--warmup W] [--game leduc-holdem] [--envs N_PER_GPU] [--T STEPS]
 """
 import argparse
@@ -54,6 +58,11 @@ def alg_bytes_per_env_step(info, T, game):
     a = 1 if info.num_actions <= 256 else 2
     return (info.obs_dim + (info.num_actions + 7) // 8 + 4 * info.num_players + 1 + 1 + a
             + 2.0 * g['state_bytes'] / T + 8.0 * g['draws_per_step'])
+
+
+def alg_bytes_philox(info, T, game):
+    """SURVEY 8(d) with R = 0 (Philox mode): the outputs and the packed state only."""
+    return alg_bytes_per_env_step(info, T, game) - 8.0 * GAMES[game]['draws_per_step']
 
 
 def precondition_launches(game, T):
@@ -170,6 +179,8 @@ def main():
                     help='N>1: trajectory exchange timed in a second phase (default: every shard into rank 0)')
     ap.add_argument('--gather-steps', type=int, default=5)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-philox', dest='philox', action='store_false',
+                    help='skip the CS_RNG_PHILOX phase (reported under "rng_philox")')
     ap.add_argument('--no-precondition', dest='precondition', action='store_false',
                     help='time from freshly seeded streams (optimistic: no MT block refills yet)')
     args = ap.parse_args()
@@ -256,6 +267,37 @@ def main():
                            bytes_per_rank_per_step=traj_bytes(traj))
         del gathered
 
+    philox_info = None
+    if args.philox and game != 'doudizhu':
+        # the engine's fast RNG mode on the same workload (not the reference's deals): own envs, same buffers
+        del env
+        penv = ShardedVecEnv(game, N, rank, seed=42, device=local, config={'rng_mode': 'philox'})
+        penv.reset()
+        for w in range(pre + args.warmup):
+            penv.rollout(T, policy_seed=5, t0=w * T, out=traj)
+        psteps = max(10, steps // 2)
+        pev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(psteps)]
+        torch.cuda.synchronize()
+        barrier()
+        p0 = time.perf_counter()
+        for k in range(psteps):
+            pev[k][0].record(stream)
+            penv.rollout(T, policy_seed=5, t0=(pre + args.warmup + k) * T, out=traj)
+            pev[k][1].record(stream)
+        torch.cuda.synchronize()
+        barrier()
+        pel = rank_max(time.perf_counter() - p0, dev)
+        pkms = sum(a.elapsed_time(b) for a, b in pev) / psteps
+        Bp = alg_bytes_philox(penv.info, T, game)
+        philox_info = dict(value=whole_job_rate(N, T, psteps, pel, world), unit='env-steps/s', steps=psteps,
+                           ms_per_step=1e3 * pel / psteps, kernel_ms_per_launch=pkms,
+                           alg_bytes_per_env_step=Bp,
+                           roofline_frac=Bp * N * T / (pkms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                           note='cs_config.rng_mode = CS_RNG_PHILOX: Philox4x32-10 byte stream keyed by the seed '
+                                'key (same games, rules and policy; not the reference deals); alg bytes = SURVEY '
+                                '8(d) with R = 0')
+        env = penv
+
     if rank == 0:
         value = whole_job_rate(N, T, steps, elapsed, world)
         B = alg_bytes_per_env_step(env.info, T, game)
@@ -292,6 +334,8 @@ def main():
                 line['roofline']['traffic_source'] = tr['source']
         if gather_info is not None:
             line['gather'] = gather_info
+        if philox_info is not None:
+            line['rng_philox'] = philox_info
         if world == 1 and not args.no_cpu_baseline:
             line['cpu_baseline'] = cpu_baseline(game)
             ref = reference_cpu(game)

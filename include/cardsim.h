@@ -38,9 +38,15 @@ typedef struct {
     int32_t num_players; /* blackjack 'game_num_players' (default 1); leduc/limit/no-limit 2; doudizhu 3 (0 = default) */
     int32_t num_decks;   /* blackjack 'game_num_decks' (default 1, 0 = infinite); ignored elsewhere (-1 = default) */
     int32_t chips_for_each; /* no-limit 'chips_for_each' (nolimitholdem/game.py:45-56): stack, 1..255 (0 = 100) */
-    int32_t dealer_plus1;   /* no-limit 'dealer_id' + 1: 0 = None (drawn by the first game, then kept), 1..2 fixed */
-    int32_t reserved[4];
+    int32_t dealer_plus1;   /* no-limit 'dealer_id' + 1: 0 = None (drawn by the first game, then kept), 1..N fixed */
+    int32_t rng_mode;       /* CS_RNG_MT19937 (0): every env draws numpy's RandomState stream of its seed, bit-exact
+                               with the reference; CS_RNG_PHILOX (1): a counter-based Philox4x32-10 byte stream keyed
+                               by the same seed key -- same games and rules, NOT the reference's deals; no MT19937
+                               state traffic (lane-per-env games; doudizhu: unsupported) */
+    int32_t reserved[3];
 } cs_config;
+
+enum { CS_RNG_MT19937 = 0, CS_RNG_PHILOX = 1 };
 
 /* Static shape of a game (rlcard Env.num_players / num_actions / state_shape). */
 typedef struct {

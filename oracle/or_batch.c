@@ -66,7 +66,10 @@ void or_batch_destroy(or_batch *b)
 
 void or_batch_seed(or_batch *b, const uint32_t *keys, const int32_t *key_len)
 {
-    for (int64_t i = 0; i < b->n; i++) or_mt_seed_by_array(&b->rng[i], keys + 2 * i, key_len[i]);
+    for (int64_t i = 0; i < b->n; i++) {
+        if (b->cfg.rng_mode == 1) or_mt_seed_philox(&b->rng[i], keys + 2 * i, key_len[i]);
+        else or_mt_seed_by_array(&b->rng[i], keys + 2 * i, key_len[i]);
+    }
 }
 
 static void *env_at(or_batch *b, int64_t i) { return b->envs + (size_t)i * b->esz; }

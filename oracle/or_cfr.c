@@ -120,7 +120,7 @@ static void traverse(or_cfr *c, uint8_t *e, const double probs[2], int player, d
 or_cfr *or_cfr_create(int64_t n, const uint32_t *keys, const int32_t *key_len)
 {
     or_cfr *c = (or_cfr *)calloc(1, sizeof(or_cfr));
-    or_cfg cfg = {2, 0, 100, -1};
+    or_cfg cfg = {2, 0, 100, -1, 0};
     c->n = n;
     c->esz = (VT->env_size(&cfg) + 15) & ~(size_t)15;
     c->envs = (uint8_t *)calloc((size_t)n, c->esz);
@@ -139,7 +139,7 @@ void or_cfr_destroy(or_cfr *c)
 
 void or_cfr_train(or_cfr *c, int32_t iterations)
 {
-    or_cfg cfg = {2, 0, 100, -1};
+    or_cfg cfg = {2, 0, 100, -1, 0};
     for (int32_t it = 0; it < iterations; it++) {
         c->iteration += 1;
         for (int p = 0; p < 2; p++) {

@@ -10,6 +10,7 @@
  * (randint), blackjack/dealer.py:23,32 (shuffle, choice), doudizhu/dealer.py:26 (shuffle).
  * Pinned by tests/golden/mt19937.npz (seeded by rlcard/utils/seeding.py:33-113) and the canonical mt19937ar vector.
  */
+#include <string.h>
 #include "oracle.h"
 
 #define MT_N 624
@@ -22,6 +23,7 @@ void or_mt_seed_int(or_mt *s, uint32_t seed)
         s->key[i] = 1812433253u * (s->key[i - 1] ^ (s->key[i - 1] >> 30)) + (uint32_t)i;
     s->pos = MT_N;
     s->ndraw = 0;
+    s->philox = 0;
 }
 
 void or_mt_seed_by_array(or_mt *s, const uint32_t *init_key, int key_length)
@@ -64,8 +66,30 @@ static void mt_gen(or_mt *s)
     s->pos = 0;
 }
 
+/* CS_RNG_PHILOX (include/cardsim.h, rlcard_amd/csrc/cs_ring.h): draw k is byte k % 16 of Philox4x32-10(key = the
+ * init_by_array key, counter = (k / 624, (k % 624) / 16)) -- the engine's ring blocks of 624 draws in 16-byte chunks.
+ * Not numpy's stream: the engine's fast mode, checked against this restatement only. */
+void or_mt_seed_philox(or_mt *s, const uint32_t *init_key, int key_length)
+{
+    memset(s, 0, sizeof(*s));
+    s->philox = 1;
+    s->pkey[0] = init_key[0];
+    s->pkey[1] = key_length == 2 ? init_key[1] : 0u;
+}
+
+static uint32_t philox_byte(or_mt *s)
+{
+    const uint64_t k = s->ndraw++, blk = k / MT_N;
+    const uint32_t j = (uint32_t)(k % MT_N) / 16u, b = (uint32_t)(k % 16u);
+    const uint32_t ctr[4] = {(uint32_t)blk, (uint32_t)(blk >> 32), j, 0u};
+    uint32_t out[4];
+    or_philox4(ctr, s->pkey, out);
+    return (out[b / 4u] >> (8u * (b % 4u))) & 255u;
+}
+
 uint32_t or_mt_next(or_mt *s)
 {
+    if (s->philox) return philox_byte(s);
     if (s->pos == MT_N) mt_gen(s);
     uint32_t y = s->key[s->pos++];
     s->ndraw++;

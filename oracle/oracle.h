@@ -26,11 +26,14 @@ typedef struct {
     uint32_t key[624];
     int32_t pos;
     uint64_t ndraw;   /* tempered u32 outputs consumed so far */
+    int32_t philox;   /* 1: the engine's CS_RNG_PHILOX byte stream (or_mt_seed_philox) instead of MT19937 */
+    uint32_t pkey[2];
 } or_mt;
 
 void or_mt_seed_int(or_mt *s, uint32_t seed);                                  /* np.random.seed(int)         */
 void or_mt_seed_by_array(or_mt *s, const uint32_t *key, int key_len);          /* RandomState().seed([...])   */
 uint32_t or_mt_next(or_mt *s);                                                 /* next tempered u32           */
+void or_mt_seed_philox(or_mt *s, const uint32_t *key, int key_len);            /* CS_RNG_PHILOX stream        */
 uint64_t or_mt_interval(or_mt *s, uint64_t max);                               /* random_interval(max)        */
 void or_mt_fill(const uint32_t *key, int key_len, uint32_t *out, int n);       /* KAT helper                  */
 void or_mt_shuffle_kat(const uint32_t *key, int key_len, const int *ns, int count, int16_t *out, int stride);
@@ -49,6 +52,7 @@ typedef struct {
     int32_t num_decks;    /* blackjack only (0 = infinite) */
     int32_t chips_for_each; /* no-limit only: stack per player (1..255) */
     int32_t dealer_id;      /* no-limit only: -1 = drawn by the first init_game, else fixed */
+    int32_t rng_mode;       /* 0 = numpy's MT19937 (the reference), 1 = the engine's CS_RNG_PHILOX stream */
 } or_cfg;
 
 typedef struct {

@@ -16,7 +16,10 @@ _ERRORS = {-1: 'CS_E_INVALID', -2: 'CS_E_DEVICE', -3: 'CS_E_STATE', -4: 'CS_E_UN
 
 class Config(C.Structure):
     _fields_ = [('num_players', C.c_int32), ('num_decks', C.c_int32), ('chips_for_each', C.c_int32),
-                ('dealer_plus1', C.c_int32), ('reserved', C.c_int32 * 4)]
+                ('dealer_plus1', C.c_int32), ('rng_mode', C.c_int32), ('reserved', C.c_int32 * 3)]
+
+
+RNG_MODES = {'mt19937': 0, 'philox': 1}   # cs_config.rng_mode
 
 
 class GameInfo(C.Structure):
@@ -113,8 +116,9 @@ def check(code, what=''):
         raise CardsimError('%s failed (%s): %s' % (what, _ERRORS.get(code, code), msg))
 
 
-def game_info(game, num_players=0, num_decks=-1, chips_for_each=0, dealer_id=None):
-    cfg = Config(num_players, num_decks, chips_for_each, 0 if dealer_id is None else int(dealer_id) + 1)
+def game_info(game, num_players=0, num_decks=-1, chips_for_each=0, dealer_id=None, rng_mode='mt19937'):
+    cfg = Config(num_players, num_decks, chips_for_each, 0 if dealer_id is None else int(dealer_id) + 1,
+                 RNG_MODES[rng_mode])
     info = GameInfo()
     check(lib().cs_game_info_get(GAME_IDS[game] if isinstance(game, str) else game, C.byref(cfg), C.byref(info)),
           'cs_game_info_get')

@@ -66,6 +66,10 @@ int cs_create(cs_handle** out, int32_t game, int64_t num_envs, int32_t device, c
     if (!out) return fail(CS_E_INVALID, "out is null");
     *out = nullptr;
     if (num_envs <= 0) return fail(CS_E_INVALID, "num_envs must be positive");
+    if (cfg && cfg->rng_mode != CS_RNG_MT19937 && cfg->rng_mode != CS_RNG_PHILOX)
+        return fail(CS_E_INVALID, "rng_mode must be CS_RNG_MT19937 or CS_RNG_PHILOX");
+    if (cfg && cfg->rng_mode == CS_RNG_PHILOX && game == CS_GAME_DOUDIZHU)
+        return fail(CS_E_UNSUPPORTED, "CS_RNG_PHILOX: lane-per-env games only (doudizhu keeps MT19937)");
     cs_game_info info;
     int r = cs_game_info_get(game, cfg, &info);
     if (r != CS_OK) return r;
@@ -87,6 +91,7 @@ int cs_create(cs_handle** out, int32_t game, int64_t num_envs, int32_t device, c
     h->b.num_decks = cfg ? cfg->num_decks : 1;
     h->b.chips_for_each = (cfg && cfg->chips_for_each > 0) ? cfg->chips_for_each : 100;
     h->b.dealer_id = cfg ? cfg->dealer_plus1 - 1 : -1;
+    h->b.rng_mode = cfg ? cfg->rng_mode : CS_RNG_MT19937;
     h->b.serial_refill = 0;
     h->b.table = nullptr;
     if ((r = set_device(h)) != CS_OK) { delete h; return r; }

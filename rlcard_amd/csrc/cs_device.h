@@ -52,6 +52,7 @@ struct GameParams {
     int32_t num_decks;
     int32_t chips_for_each;   // no-limit: stack per player
     int32_t dealer_id;        // no-limit: -1 = drawn by the first reset (rlcard's None), else fixed
+    int32_t rng_mode;         // CS_RNG_MT19937 (reference-compatible) or CS_RNG_PHILOX (cs_ring.h)
 };
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y)

@@ -20,6 +20,7 @@ struct Buffers {
     int32_t num_players, num_decks;
     int32_t chips_for_each, dealer_id;   // no-limit hold'em (cs_config; dealer_id -1 = drawn)
     int32_t serial_refill;  // testing hook
+    int32_t rng_mode;       // cs_config.rng_mode
     int32_t obs_dim, num_actions, action_bytes;   // cs_game_info of the handle
 };
 

@@ -16,6 +16,12 @@
 // wave refills at step boundaries (ring_refill_wave); a lane that would step past L inside a step (more than 624
 // draws in one step: only a rejection loop's tail) generates in-lane (ring_gen_serial): slow, never on the fast path,
 // same numbers.
+//
+// Philox mode (cs_config.rng_mode = CS_RNG_PHILOX, ctl bit 18; not seed-compatible with the reference): the ring
+// layout, staging and every game's draw code stay as they are, but a refill fills the three slots with Philox4x32-10
+// bytes -- key = the env's init_by_array key, counter = (absolute block index, 16-byte chunk) -- instead of twisting:
+// wbuf holds only the block counter and the key (words 0..2), so the refill reads nothing and writes 1 872 ring bytes
+// (~2 B per draw: written once, read once) where MT19937 moves ~4.7.
 #pragma once
 #include "cs_device.h"
 
@@ -24,6 +30,8 @@ namespace cs {
 constexpr int RING_SLOTS = 4;
 constexpr int RING_GEN = RING_SLOTS - 1;        // blocks generated per refill
 constexpr uint32_t RING = RING_SLOTS * MT_N;    // 2 496 bytes
+constexpr uint32_t CTL_PHILOX = 1u << 18;       // ctl bit: the env's stream is the Philox byte stream
+constexpr int PHX_CHUNKS = MT_N / 16;           // 39 Philox blocks (16 bytes) per ring block
 
 __device__ __forceinline__ uint32_t shfl(uint32_t v, int src_lane)
 {
@@ -50,9 +58,31 @@ __device__ inline void ring_bytes_serial(const uint32_t* w, uint8_t* ring, uint3
     }
 }
 
-// one lane generates blocks L+1..L+3 after L (slot lat): the rare in-step path and seeding
-__device__ __attribute__((noinline)) void ring_gen_serial(uint32_t* wbuf, uint32_t lat)
+// Philox mode: chunks c0, c0 + step, .. of the next RING_GEN blocks after slot lat (chunk c = 16 bytes: block c / 39,
+// 16-byte piece c % 39), counter (block index wbuf[0] + c / 39, c % 39), key wbuf[1..2]. The caller advances wbuf[0].
+__device__ __forceinline__ void ring_gen_philox(gu32* wbuf, uint32_t lat, int c0, int step)
 {
+    const uint32_t blk0 = wbuf[0];
+    const uint64_t key = (uint64_t)wbuf[1] | (uint64_t)wbuf[2] << 32;
+    gu32* ring = wbuf + MT_N;
+    for (int c = c0; c < RING_GEN * PHX_CHUNKS; c += step) {
+        const int b = c / PHX_CHUNKS, j = c - b * PHX_CHUNKS;
+        uint32_t w[4];
+        philox4(key, (uint64_t)(blk0 + (uint32_t)b), (uint64_t)j, w);
+        const uint32_t slot = (lat + 1u + (uint32_t)b) & 3u;
+        gu32* d = ring + slot * (MT_N / 4) + 4 * j;
+        d[0] = w[0]; d[1] = w[1]; d[2] = w[2]; d[3] = w[3];
+    }
+}
+
+// one lane generates blocks L+1..L+3 after L (slot lat): the rare in-step path and seeding
+__device__ __attribute__((noinline)) void ring_gen_serial(uint32_t* wbuf, uint32_t lat, uint32_t phx = 0)
+{
+    if (phx) {
+        ring_gen_philox((gu32*)wbuf, lat, 0, 1);
+        wbuf[0] += (uint32_t)RING_GEN;
+        return;
+    }
     uint8_t* ring = (uint8_t*)(wbuf + MT_N);
     for (uint32_t b = 1; b <= (uint32_t)RING_GEN; b++) {
         mt_twist_inplace(wbuf);
@@ -110,8 +140,14 @@ __device__ __forceinline__ void ring_st(gu32* p, uint32_t v)
 }
 
 // Wave-cooperative refill of one env: blocks L+1..L+3 from wbuf (block L, slot lat). All 64 lanes must call.
-__device__ __forceinline__ void ring_gen_wave(gu32* wbuf, uint32_t lat, int lane)
+__device__ __forceinline__ void ring_gen_wave(gu32* wbuf, uint32_t lat, int lane, uint32_t phx = 0)
 {
+    if (phx) {   // Philox mode: 117 chunks over the 64 lanes, then the block counter (read by every lane first)
+        const uint32_t blk0 = wbuf[0];
+        ring_gen_philox(wbuf, lat, lane, WAVE);
+        if (lane == 0) wbuf[0] = blk0 + (uint32_t)RING_GEN;
+        return;
+    }
     uint32_t o[10], n[10];
 #pragma unroll
     for (int c = 0; c < 10; c++) o[c] = (c < 9 || lane < 48) ? ring_ld(wbuf + 64 * c + lane) : 0u;
@@ -146,17 +182,19 @@ struct RingLane {
     uint32_t lat;     // slot of the latest generated block
     uint32_t sp, sn;  // ring position of staged byte 0; staged bytes
     const uint8_t* stg;
+    uint32_t phx;     // CTL_PHILOX when the env's stream is the Philox byte stream
 
     __device__ __forceinline__ void init(uint32_t* p_base, uint32_t ctlw)
     {
         base = p_base;
         pos = ctlw & 0xFFFu;
         lat = (ctlw >> 12) & 3u;
+        phx = ctlw & CTL_PHILOX;
         sp = 0;
         sn = 0;
         stg = nullptr;
     }
-    __device__ __forceinline__ uint32_t ctl_word() const { return pos | lat << 12; }
+    __device__ __forceinline__ uint32_t ctl_word() const { return pos | lat << 12 | phx; }
     __device__ __forceinline__ const uint8_t* ring() const { return (const uint8_t*)(base + MT_N); }
     __device__ __forceinline__ uint32_t limit() const { return ((lat + 1u) & 3u) * (uint32_t)MT_N; }
     // draws left before the end of the generated data (1 .. RING)
@@ -169,7 +207,7 @@ struct RingLane {
 
     __device__ __forceinline__ void gen_serial()
     {
-        ring_gen_serial(base, lat);
+        ring_gen_serial(base, lat, phx);
         lat = (lat + (uint32_t)RING_GEN) & 3u;
     }
 
@@ -312,7 +350,8 @@ __device__ __forceinline__ void ring_refill_wave(M& m, int lane)
     while (need) {
         const int j = __builtin_ctzll(need);
         need &= need - 1;
-        ring_gen_wave(lane_ptr(m.base, j), __builtin_amdgcn_readlane(m.lat, j), lane);
+        ring_gen_wave(lane_ptr(m.base, j), __builtin_amdgcn_readlane(m.lat, j), lane,
+                      __builtin_amdgcn_readlane(m.phx, j));
         if (lane == j) m.lat = (m.lat + (uint32_t)RING_GEN) & 3u;
     }
     // the ring bytes are read later by their owner lane of this same wave: order the stores before those loads

@@ -311,17 +311,25 @@ __global__ __launch_bounds__(BLOCK) void k_seed(uint32_t* mt, uint32_t* ctl, uin
         if (!valid) return;
         uint32_t* wbuf = mt + env * MT_WORDS;
         const int kl = klen[i] == 2 ? 2 : 1;                    // validated on the host; never trust it here
-        mt_init_by_array(wbuf, keys + 2 * i, kl);
-        for (uint32_t b = 0; b < (uint32_t)RING_GEN; b++) {     // numpy's first draws: block 0 = twist(S0)
-            mt_twist_inplace(wbuf);
-            ring_bytes_serial(wbuf, (uint8_t*)(wbuf + MT_N), b);
+        const uint32_t phx = prm.rng_mode == CS_RNG_PHILOX ? CTL_PHILOX : 0u;
+        if (phx) {   // Philox byte stream: block counter 0, key = the init_by_array key, blocks 0..2 into slots 0..2
+            wbuf[0] = 0u;
+            wbuf[1] = keys[2 * i];
+            wbuf[2] = kl == 2 ? keys[2 * i + 1] : 0u;
+            ring_gen_serial(wbuf, 3u, phx);
+        } else {
+            mt_init_by_array(wbuf, keys + 2 * i, kl);
+            for (uint32_t b = 0; b < (uint32_t)RING_GEN; b++) {     // numpy's first draws: block 0 = twist(S0)
+                mt_twist_inplace(wbuf);
+                ring_bytes_serial(wbuf, (uint8_t*)(wbuf + MT_N), b);
+            }
         }
         G g;
         g.bind(scratch_of<G>(scr[threadIdx.x / WAVE], lane), prm);
         g.blank();
         g.store(st, n, env);
         if constexpr (DqOf<G>::value > 0) st[(int64_t)G::GW * n + env] = 0u;   // empty deal queue
-        ctl[env] = 0u | (uint32_t)(RING_GEN - 1) << 12;          // position 0, latest block in slot 2
+        ctl[env] = 0u | (uint32_t)(RING_GEN - 1) << 12 | phx;    // position 0, latest block in slot 2
         return;
     }
     MtLane m;
@@ -577,7 +585,7 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
 // ------------------------------------------------------------------------------------------------------------------
 static inline GameParams params_of(const Buffers& b)
 {
-    return GameParams{b.num_players, b.num_decks, b.chips_for_each, b.dealer_id};
+    return GameParams{b.num_players, b.num_decks, b.chips_for_each, b.dealer_id, b.rng_mode};
 }
 static inline dim3 grid_for(int64_t n, int epw = WAVE)
 {

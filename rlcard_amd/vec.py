@@ -58,7 +58,8 @@ class VecEnv:
         np_ = int(config.get('game_num_players', 0))
         nd = int(config.get('game_num_decks', -1))
         chips = int(config.get('chips_for_each', 0))
-        self.info, self.cfg = _abi.game_info(self.game, np_, nd, chips, config.get('dealer_id'))
+        self.rng_mode = config.get('rng_mode', 'mt19937')   # 'philox': fast, not the reference's deals
+        self.info, self.cfg = _abi.game_info(self.game, np_, nd, chips, config.get('dealer_id'), self.rng_mode)
         self.obs_dim = self.info.obs_dim
         self.num_actions = self.info.num_actions
         self.num_players = self.info.num_players

@@ -22,12 +22,13 @@ def build():
 
 
 class MT(C.Structure):
-    _fields_ = [('key', C.c_uint32 * 624), ('pos', C.c_int32), ('ndraw', C.c_uint64)]
+    _fields_ = [('key', C.c_uint32 * 624), ('pos', C.c_int32), ('ndraw', C.c_uint64), ('philox', C.c_int32),
+                ('pkey', C.c_uint32 * 2)]
 
 
 class Cfg(C.Structure):
     _fields_ = [('num_players', C.c_int32), ('num_decks', C.c_int32), ('chips_for_each', C.c_int32),
-                ('dealer_id', C.c_int32)]
+                ('dealer_id', C.c_int32), ('rng_mode', C.c_int32)]
 
 
 class Info(C.Structure):
@@ -94,11 +95,12 @@ def load_ddz_table():
 class Batch:
     """Oracle batch with the C-ABI semantics; outputs as numpy arrays."""
 
-    def __init__(self, game, n, keys, key_len, num_players=None, num_decks=1, chips_for_each=100, dealer_id=-1):
+    def __init__(self, game, n, keys, key_len, num_players=None, num_decks=1, chips_for_each=100, dealer_id=-1,
+                 rng_mode=0):
         L = lib()
         self.game = GAMES[game] if isinstance(game, str) else game
         np_ = num_players if num_players is not None else {0: 1, 1: 2, 2: 2, 3: 3, 4: 2}[self.game]
-        self.cfg = Cfg(np_, num_decks, chips_for_each, dealer_id)
+        self.cfg = Cfg(np_, num_decks, chips_for_each, dealer_id, rng_mode)
         self.info = Info()
         if L.or_game_info(self.game, C.byref(self.cfg), C.byref(self.info)) != 0:
             raise ValueError('bad game config')

@@ -1,0 +1,68 @@
+"""CS_RNG_PHILOX (cs_config.rng_mode, rlcard_amd/csrc/cs_ring.h): the engine's fast, non-seed-compatible stream.
+Same games and rules over a Philox4x32-10 byte stream; checked against the oracle running the same stream
+(oracle/or_rng.c or_mt_seed_philox), past several ring refills. Needs a GPU."""
+import numpy as np
+import pytest
+
+from rlcard_amd import seeding
+
+torch = pytest.importorskip('torch')
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail('GPU tests need a visible GPU (run them on the MI355X box)')
+
+
+def _np(o):
+    return {k: v.cpu().numpy() for k, v in o.items()}
+
+
+def _same(got, exp, what):
+    for k in exp:
+        if k not in got:
+            continue
+        g, e = got[k], exp[k].astype(got[k].dtype)
+        if not np.array_equal(g, e):
+            bad = np.argwhere(g != e)
+            raise AssertionError('%s: %s differs at %d places, first %s' % (what, k, len(bad), bad[0]))
+
+
+@pytest.mark.parametrize('game,cfg,T', [('leduc-holdem', {}, 512), ('limit-holdem', {}, 64),
+                                        ('no-limit-holdem', {}, 64), ('blackjack', {}, 32),
+                                        ('leduc-holdem', {'game_num_players': 3}, 768),
+                                        ('limit-holdem', {'game_num_players': 4}, 64)])
+@pytest.mark.parametrize('flags', [0, 1])
+def test_philox_stream_matches_oracle(oracle, game, cfg, T, flags):
+    from rlcard_amd import VecEnv
+    n = 2000 + 11
+    v = VecEnv(game, n, seed=21, config=dict(cfg, rng_mode='philox'))
+    v.set_kernel_flags(flags)
+    keys, lens = seeding.seed_keys(range(21, 21 + n))
+    ob = oracle.Batch(game, n, keys, lens, num_players=cfg.get('game_num_players'), rng_mode=1)
+    _same(_np(v.reset()), ob.reset(), 'reset')
+    rng = np.random.RandomState(2)
+    for t in range(20):
+        acts = rng.randint(0, v.num_actions, size=n).astype(np.int32)
+        _same(_np(v.step(torch.from_numpy(acts).cuda())), ob.step(acts), 'step %d' % t)
+    for c in range(3):
+        _same(_np(v.rollout(T, policy_seed=8, t0=c * T)), ob.rollout(T, 8, c * T, 0), 'rollout %d' % c)
+    torch.cuda.synchronize()
+    for i in (0, 64, n - 1):
+        assert v.rng_position(i) == ob.draws(i) % v.rng_period
+    assert max(ob.draws(i) for i in range(0, n, 97)) > 1248 + 624, 'the test crosses ring refills'
+
+
+def test_philox_deals_differ_from_mt19937():
+    from rlcard_amd import VecEnv
+    a = VecEnv('leduc-holdem', 256, seed=1)
+    b = VecEnv('leduc-holdem', 256, seed=1, config={'rng_mode': 'philox'})
+    assert not torch.equal(a.reset()['obs'], b.reset()['obs'])
+
+
+def test_philox_refused_for_doudizhu():
+    from rlcard_amd import VecEnv, _abi
+    with pytest.raises(_abi.CardsimError):
+        VecEnv('doudizhu', 8, config={'rng_mode': 'philox'})

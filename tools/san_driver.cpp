@@ -68,7 +68,7 @@ static void oracle_games()
     const int games[] = {OR_BLACKJACK, OR_LEDUC, OR_LIMIT, OR_DOUDIZHU, OR_NOLIMIT};
     for (int g : games) {
         for (int variant = 0; variant < 2; variant++) {
-            or_cfg cfg = {0, 1, 100, -1};
+            or_cfg cfg = {0, 1, 100, -1, 0};
             cfg.num_players = g == OR_BLACKJACK ? (variant ? 3 : 1) : (g == OR_DOUDIZHU ? 3 : 2);
             if (g == OR_BLACKJACK && variant) cfg.num_decks = 0;
             if (g == OR_NOLIMIT && variant) { cfg.chips_for_each = 7; cfg.dealer_id = 1; }
