@@ -227,6 +227,14 @@ int cs_get_env_state(cs_handle* h, int64_t env, uint32_t* host_words, int32_t nw
  * Env: one packed device-to-host copy per Env.step, envs/env.py:65-86). */
 int cs_copy_env_state(cs_handle* h, int64_t env, uint32_t* dst, void* stream);
 
+/* Single-env completion without a stream synchronisation (rlcard_amd.make's Env: one launch and a spin per Env.step):
+ * when seq is not NULL, every later cs_reset / cs_step / cs_observe also writes env `env`'s packed state words to
+ * `words` (state_words u32, 16-byte aligned) and then -- after a system-scope fence ordering all of that env's output
+ * stores -- the call's sequence number to *seq: 1 for the first call after cs_set_step_record, then 2, 3, ... Both
+ * are device-visible pointers, typically mapped pinned host memory the host polls. seq NULL turns it off. Only that
+ * env's outputs are covered; meant for single-env handles. */
+int cs_set_step_record(cs_handle* h, int64_t env, uint32_t* words, uint32_t* seq);
+
 /* Overwrite the packed state words of env `env` from a HOST buffer taken by cs_get_env_state: Env.step_back
  * (envs/env.py:88-108) restores the game from its history. The env's RNG stream is left where it is, as the
  * reference's np_random is not part of the restored history. Synchronous. */

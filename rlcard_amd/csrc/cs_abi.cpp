@@ -92,6 +92,7 @@ int cs_create(cs_handle** out, int32_t game, int64_t num_envs, int32_t device, c
     h->b.chips_for_each = (cfg && cfg->chips_for_each > 0) ? cfg->chips_for_each : 100;
     h->b.dealer_id = cfg ? cfg->dealer_plus1 - 1 : -1;
     h->b.rng_mode = cfg ? cfg->rng_mode : CS_RNG_MT19937;
+    h->b.rec = cs::StepRecord{nullptr, nullptr, 0u, 0};
     h->b.serial_refill = 0;
     h->b.table = nullptr;
     if ((r = set_device(h)) != CS_OK) { delete h; return r; }
@@ -174,6 +175,7 @@ int cs_reset(cs_handle* h, const cs_step_out* out, void* stream)
     if (!h->seeded) return fail(CS_E_STATE, "cs_reset before cs_seed");
     int r = set_device(h);
     if (r != CS_OK) return r;
+    if (h->b.rec.seq) h->b.rec.seqv++;
     hipError_t e = cs::launch_reset(h->b, *out, (hipStream_t)stream);
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_reset");
 }
@@ -184,6 +186,7 @@ int cs_step(cs_handle* h, const int32_t* actions, const cs_step_out* out, void* 
     if (!h->seeded) return fail(CS_E_STATE, "cs_step before cs_seed");
     int r = set_device(h);
     if (r != CS_OK) return r;
+    if (h->b.rec.seq) h->b.rec.seqv++;
     hipError_t e = cs::launch_step(h->b, actions, *out, (hipStream_t)stream);
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_step");
 }
@@ -194,8 +197,18 @@ int cs_observe(cs_handle* h, int32_t player, const cs_step_out* out, void* strea
     if (player < 0 || player >= h->info.num_players) return fail(CS_E_INVALID, "player out of range");
     int r = set_device(h);
     if (r != CS_OK) return r;
+    if (h->b.rec.seq) h->b.rec.seqv++;
     hipError_t e = cs::launch_observe(h->b, player, *out, (hipStream_t)stream);
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_observe");
+}
+
+int cs_set_step_record(cs_handle* h, int64_t env, uint32_t* words, uint32_t* seq)
+{
+    if (!h) return fail(CS_E_INVALID, "null argument");
+    if (seq && (!words || env < 0 || env >= h->b.n)) return fail(CS_E_INVALID, "words / env out of range");
+    if (words && ((uintptr_t)words & 15u)) return fail(CS_E_INVALID, "words must be 16-byte aligned");
+    h->b.rec = cs::StepRecord{seq ? words : nullptr, seq, 0u, seq ? env : 0};
+    return CS_OK;
 }
 
 int cs_cfr_train(cs_handle* h, int32_t iterations, int64_t iteration0, double* policy, double* average_policy,

@@ -637,7 +637,7 @@ __device__ __forceinline__ void payoffs(const Env& e, float* r)   // judger.py:3
 }
 
 __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
-                                                  cs_step_out out, Tab tb)
+                                                  cs_step_out out, Tab tb, StepRecord rec)
 {
     __shared__ WaveLds lds[WPB];
     __shared__ TabLds tl;
@@ -655,10 +655,15 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, ui
     }
     e.store(st, c.env, c.lane);
     if (c.lane == 0) ctl[c.env] = m.pos | (m.stale << 16);
+    if (rec.seq != nullptr && c.env == rec.env) {   // StepRecord (cs_engine.h): state words, fence, sequence number
+        e.store(rec.words, 0, c.lane);
+        __threadfence_system();
+        if (c.lane == 0) __hip_atomic_store(rec.seq, rec.seqv, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
-                                                 const int32_t* actions, cs_step_out out, Tab tb)
+                                                 const int32_t* actions, cs_step_out out, Tab tb, StepRecord rec)
 {
     __shared__ WaveLds lds[WPB];
     __shared__ TabLds tl;
@@ -689,9 +694,15 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uin
     }
     e.store(st, c.env, c.lane);
     if (c.lane == 0) ctl[c.env] = m.pos | (m.stale << 16);
+    if (rec.seq != nullptr && c.env == rec.env) {   // StepRecord (cs_engine.h): state words, fence, sequence number
+        e.store(rec.words, 0, c.lane);
+        __threadfence_system();
+        if (c.lane == 0) __hip_atomic_store(rec.seq, rec.seqv, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n, int player, cs_step_out out, Tab tb)
+__global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n, int player, cs_step_out out, Tab tb,
+                                                    StepRecord rec)
 {
     __shared__ WaveLds lds[WPB];
     __shared__ TabLds tl;
@@ -701,6 +712,11 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n
     Env e;
     e.load(st, c.env, c.lane, tb);
     emit_state(e, (uint32_t)player, tb, tl, lds[c.wid], c.lane, c.env, out);
+    if (rec.seq != nullptr && c.env == rec.env) {   // StepRecord (cs_engine.h): state words, fence, sequence number
+        e.store(rec.words, 0, c.lane);
+        __threadfence_system();
+        if (c.lane == 0) __hip_atomic_store(rec.seq, rec.seqv, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 __global__ __launch_bounds__(BLOCK, CS_DDZ_MINW) void k_rollout(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n, int T,
@@ -827,18 +843,19 @@ hipError_t launch_debug_legal(const Buffers& b, const uint8_t* counts, const int
 
 hipError_t launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_reset, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, o, *(const Tab*)b.table);
+    hipLaunchKernelGGL(k_reset, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, o, *(const Tab*)b.table,
+                       b.rec);
     return hipGetLastError();
 }
 hipError_t launch_step(const Buffers& b, const int32_t* a, const cs_step_out& o, hipStream_t s)
 {
     hipLaunchKernelGGL(k_step, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, a, o,
-                       *(const Tab*)b.table);
+                       *(const Tab*)b.table, b.rec);
     return hipGetLastError();
 }
 hipError_t launch_observe(const Buffers& b, int32_t p, const cs_step_out& o, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_observe, grid_of(b.n), dim3(BLOCK), 0, s, b.state, b.n, p, o, *(const Tab*)b.table);
+    hipLaunchKernelGGL(k_observe, grid_of(b.n), dim3(BLOCK), 0, s, b.state, b.n, p, o, *(const Tab*)b.table, b.rec);
     return hipGetLastError();
 }
 hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,

@@ -8,6 +8,16 @@ namespace cs {
 
 constexpr int MT_WORDS_HOST = 2 * 624;  // u32 per env: two MT19937 blocks
 
+// cs_set_step_record: the single-step kernels also write env `env`'s packed state words to `words`, then -- after a
+// system-scope fence that orders every output store of that env's wave -- `seqv` to *seq (both typically in mapped
+// host memory), so a single-env host can spin on *seq instead of synchronising the stream
+struct StepRecord {
+    uint32_t* words;
+    uint32_t* seq;
+    uint32_t seqv;
+    int64_t env;
+};
+
 struct Buffers {
     int32_t game;
     int64_t n;
@@ -21,6 +31,7 @@ struct Buffers {
     int32_t chips_for_each, dealer_id;   // no-limit hold'em (cs_config; dealer_id -1 = drawn)
     int32_t serial_refill;  // testing hook
     int32_t rng_mode;       // cs_config.rng_mode
+    StepRecord rec;         // seq == nullptr: off
     int32_t obs_dim, num_actions, action_bytes;   // cs_game_info of the handle
 };
 

@@ -291,6 +291,20 @@ __device__ __forceinline__ void game_reset(G& g, Rng& rng, uint32_t* st, int64_t
     }
 }
 
+// StepRecord (cs_engine.h): the wave holding env rec.env writes its state words and, after a system-scope fence (it
+// waits for every store the wave issued: its obs rows, legal bytes, player, reward, done), the sequence number
+template <class G>
+__device__ __forceinline__ void step_record(const StepRecord& rec, const uint32_t* st, int64_t n, const LaneCtx& c)
+{
+    if (rec.seq == nullptr || rec.env < c.wave_first || rec.env >= c.wave_first + WAVE) return;   // wave-uniform
+    if (c.valid && c.env == rec.env) {
+#pragma unroll
+        for (int w = 0; w < G::WORDS; w++) rec.words[w] = st[(int64_t)w * n + c.env];
+    }
+    __threadfence_system();
+    if (c.valid && c.env == rec.env) __hip_atomic_store(rec.seq, rec.seqv, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 #define CS_SMEM_ROWS(G, ROWS)                                         \
     __shared__ uint32_t lds[WAVES_PER_BLOCK][ObsLds<G, ROWS>::WORDS]; \
     __shared__ uint32_t scr[WAVES_PER_BLOCK][Scratch<G>::WORDS]
@@ -357,7 +371,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed(uint32_t* mt, uint32_t* ctl, uin
 
 template <class G>
 __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
-                                                  cs_step_out out, int flags, GameParams prm)
+                                                  cs_step_out out, int flags, GameParams prm, StepRecord rec)
 {
     CS_SMEM(G);
     const LaneCtx c = lane_ctx(n);
@@ -387,12 +401,13 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, ui
         g.store(st, n, c.env);
         ctl[c.env] = m.ctl_word();
     }
+    step_record<G>(rec, st, n, c);
 }
 
 template <class G>
 __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
                                                  const int32_t* actions, cs_step_out out, int flags,
-                                                 GameParams prm)
+                                                 GameParams prm, StepRecord rec)
 {
     CS_SMEM(G);
     const LaneCtx c = lane_ctx(n);
@@ -427,11 +442,12 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uin
         g.store(st, n, c.env);
         ctl[c.env] = m.ctl_word();
     }
+    step_record<G>(rec, st, n, c);
 }
 
 template <class G>
 __global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n, int player, cs_step_out out,
-                                                    GameParams prm)
+                                                    GameParams prm, StepRecord rec)
 {
     CS_SMEM(G);
     const LaneCtx c = lane_ctx(n);
@@ -447,6 +463,7 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n
         if (out.player) ((uint8_t*)out.player)[c.env] = (uint8_t)g.current();
         if (out.done) ((uint8_t*)out.done)[c.env] = (uint8_t)g.is_over();
     }
+    step_record<G>(rec, st, n, c);
 }
 
 template <class G>
@@ -604,20 +621,21 @@ static hipError_t seed_g(const Buffers& b, const uint32_t* keys, const int32_t* 
 template <class G>
 static hipError_t reset_g(const Buffers& b, const cs_step_out& o, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_reset<G>, grid_for(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, o, b.serial_refill, params_of(b));
+    hipLaunchKernelGGL(k_reset<G>, grid_for(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, o, b.serial_refill,
+                       params_of(b), b.rec);
     return hipGetLastError();
 }
 template <class G>
 static hipError_t step_g(const Buffers& b, const int32_t* a, const cs_step_out& o, hipStream_t s)
 {
     hipLaunchKernelGGL(k_step<G>, grid_for(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, a, o, b.serial_refill,
-                       params_of(b));
+                       params_of(b), b.rec);
     return hipGetLastError();
 }
 template <class G>
 static hipError_t observe_g(const Buffers& b, int32_t p, const cs_step_out& o, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_observe<G>, grid_for(b.n), dim3(BLOCK), 0, s, b.state, b.n, p, o, params_of(b));
+    hipLaunchKernelGGL(k_observe<G>, grid_for(b.n), dim3(BLOCK), 0, s, b.state, b.n, p, o, params_of(b), b.rec);
     return hipGetLastError();
 }
 template <class G>

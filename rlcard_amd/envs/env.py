@@ -6,11 +6,12 @@ get_payoffs/is_over/get_player_id/seed/timestep/action_recorder, state dicts {'o
 rlcard.make() runs unchanged. Every game rule, deal and observation is computed by the kernels; this layer only
 converts one row of the engine's outputs into the reference's Python types. Throughput belongs to VecEnv.
 
-Per Env.step the host makes one round trip: the step kernel writes the env's outputs (reward, obs, legal bitmask,
-player, done) and cs_copy_env_state the packed state words (the raw_obs fields) straight into one record of mapped
-host memory, on the env's own stream; one stream synchronisation later the host decodes it (_Io).
+Per Env.step the host makes one round trip: one step kernel writes the env's outputs (reward, obs, legal bitmask,
+player, done) and its packed state words (the raw_obs fields) straight into one record of mapped host memory, then
+a sequence number the host spins on (cs_set_step_record, _Io); the host decodes the record.
 """
 import ctypes as C
+import time
 from collections import OrderedDict
 
 import numpy as np
@@ -35,20 +36,25 @@ def _hip_lib():
 
 
 HIP_HOST_MALLOC_MAPPED, HIP_HOST_MALLOC_COHERENT = 0x2, 0x40000000
+_BYTE_IDS = [tuple(i for i in range(8) if (b >> i) & 1) for b in range(256)]   # legal bitmask byte -> ids
 
 
 class _Io:
-    """One env's step record, written by the kernels straight into mapped (device-visible, coherent) pinned host
-    memory: reward f32 [P] | state words u32 [S] | obs u8 [O] | legal u8 [LB] | player u8 | done u8. Actions come
-    from a constant device table of every action id (the step reads actions[0] at &table[a]), so a step is two
-    launches on the env's own stream and one stream synchronisation -- no uploads, no copies."""
+    """One env's step record in mapped (device-visible, coherent) pinned host memory, written by the step kernels
+    themselves (cs_set_step_record): seq u32 | pad | state words u32 [S] (16-B aligned) | reward f32 [P] | obs u8 [O]
+    | legal u8 [LB] | player u8 | done u8. Actions come from a constant device table of every action id (a step reads
+    actions[0] at &table[a]). So an Env.step is one launch on the env's own stream and a spin on seq -- no stream
+    synchronisation, no uploads, no copies."""
+
+    SPIN_S = 0.002   # past this the wait falls back to hipStreamSynchronize (and reports a launch failure)
 
     def __init__(self, vec):
         i = vec.info
         P, S, O, LB = i.num_players, i.state_words, i.obs_dim, i.legal_bytes
         self.P, self.S, self.O, self.LB = P, S, O, LB
-        self.o_words = 4 * P
-        self.o_obs = self.o_words + 4 * S
+        self.o_words = 16
+        self.o_reward = self.o_words + (4 * S + 15) // 16 * 16
+        self.o_obs = self.o_reward + 4 * P
         self.o_legal = self.o_obs + O
         self.o_player = self.o_legal + LB
         self.o_done = self.o_player + 1
@@ -65,20 +71,35 @@ class _Io:
                 raise _abi.CardsimError('hipHostGetDevicePointer of the step record failed')
         self.np = np.frombuffer((C.c_uint8 * total).from_address(hp.value), dtype=np.uint8)
         self.np[:] = 0
+        self.seq = self.np[:4].view(np.uint32)
         base = dp.value
         self.st = C.c_void_p(self.stream.cuda_stream)
         self.out = _abi.StepOut(C.c_void_p(base + self.o_obs), C.c_void_p(base + self.o_legal),
-                                C.c_void_p(base + self.o_player), C.c_void_p(base), C.c_void_p(base + self.o_done))
+                                C.c_void_p(base + self.o_player), C.c_void_p(base + self.o_reward),
+                                C.c_void_p(base + self.o_done))
         self.obs_out = _abi.StepOut(self.out.obs, self.out.legal, self.out.player, None, self.out.done)
-        self.words_ptr = C.c_void_p(base + self.o_words)
         self.ids_base = self.ids.data_ptr()
+        _abi.check(_abi.lib().cs_set_step_record(vec._h, 0, C.c_void_p(base + self.o_words), C.c_void_p(base)),
+                   'cs_set_step_record')
+        self.expect = 0
 
     def act_ptr(self, a):
         return C.c_void_p(self.ids_base + 4 * a)
 
-    def sync(self):
-        if _hip.hipStreamSynchronize(self.st) != 0:
-            raise _abi.CardsimError('hipStreamSynchronize failed: %s' % _abi.lib().cs_last_error().decode())
+    def wait(self):
+        """Spin until the kernel has published this call's record (seq), else synchronise and report."""
+        self.expect = (self.expect + 1) & 0xFFFFFFFF
+        seq, want = self.seq, self.expect
+        if seq[0] == want:
+            return
+        t0 = time.perf_counter()
+        while seq[0] != want:
+            if time.perf_counter() - t0 > self.SPIN_S:
+                if _hip.hipStreamSynchronize(self.st) != 0:
+                    raise _abi.CardsimError('hipStreamSynchronize failed: %s' % _abi.lib().cs_last_error().decode())
+                if seq[0] != want:
+                    raise _abi.CardsimError('step record not published (seq %d, expected %d)' % (seq[0], want))
+                return
 
     def close(self):
         if getattr(self, '_hp', None) is not None and self._hp.value:
@@ -96,8 +117,8 @@ class _Io:
         out = {'obs': h[self.o_obs:self.o_obs + self.O].copy(), 'legal': h[self.o_legal:self.o_legal + self.LB].copy(),
                'player': int(h[self.o_player]), 'done': bool(h[self.o_done])}
         if with_reward:
-            out['reward'] = h[:self.o_words].view(np.float32).copy()
-        words = h[self.o_words:self.o_obs].view(np.uint32).tolist()
+            out['reward'] = h[self.o_reward:self.o_obs].view(np.float32).copy()
+        words = h[self.o_words:self.o_words + 4 * self.S].view(np.uint32).tolist()
         return out, words
 
 
@@ -139,8 +160,7 @@ class Env(object):
             _abi.check(L.cs_reset(h, C.byref(io.out), io.st), 'cs_reset')
         else:
             _abi.check(L.cs_observe(h, int(arg), C.byref(io.obs_out), io.st), 'cs_observe')
-        _abi.check(L.cs_copy_env_state(h, 0, io.words_ptr, io.st), 'cs_copy_env_state')
-        io.sync()
+        io.wait()
         out, self._words = io.record(with_reward)
         return out
 
@@ -250,7 +270,10 @@ class Env(object):
 
     # -- engine row -> reference types ---------------------------------------------------------------------------
     def _legal_ids(self, out):
-        return legal_ids(out['legal'])
+        lg = out['legal']
+        if len(lg) == 1:   # one bitmask byte (every game but doudizhu): table lookup
+            return list(_BYTE_IDS[int(lg[0])])
+        return legal_ids(lg)
 
     def _extract_state(self, out, player_id):
         ids = self._legal_ids(out)
