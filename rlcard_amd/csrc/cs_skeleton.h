@@ -132,14 +132,45 @@ __device__ __forceinline__ void emit_legal(uint8_t* legal, int64_t row, uint64_t
     for (int k = 0; k < G::LB; k++) out_store(legal + row * G::LB + k, (uint8_t)(lg >> (8 * k)));
 }
 
+#ifndef CS_REWARD_NT
+#define CS_REWARD_NT 1   // 0: default-policy 8-B reward stores (A/B knob)
+#endif
 template <class G>
 __device__ __forceinline__ void emit_reward(float* reward, int64_t row, const float (&r)[G::P])
 {
     if constexpr (G::P == 2) {
-        out_store((uint64_t*)(reward + row * 2), (uint64_t)__float_as_uint(r[0]) | (uint64_t)__float_as_uint(r[1]) << 32);
+        const uint64_t v = (uint64_t)__float_as_uint(r[0]) | (uint64_t)__float_as_uint(r[1]) << 32;
+        if constexpr (CS_REWARD_NT) out_store((uint64_t*)(reward + row * 2), v);
+        else *(uint64_t*)(reward + row * 2) = v;
     } else {
 #pragma unroll
         for (int k = 0; k < G::P; k++) reward[row * G::P + k] = r[k];
+    }
+}
+
+// Two-player reward rows (8 B) of the rollout as 16-B stores: even lanes take their odd neighbour's pair (one DPP
+// row shift) and store both rows at once. All lanes call (invalid lanes hold zeros). CS_REWARD_PAIRS=0: one 8-B store
+// per lane. Measured: the 8-B nontemporal reward rows cost ~1.8x their bytes in WRITE_SIZE (Leduc 1.6 GB
+// per launch); pairs bring WRITE_SIZE to the algorithmic bytes but ran slower (4.59 -> 4.78 ms Leduc, 2.67 -> 2.80
+// Limit, same box): off.
+#ifndef CS_REWARD_PAIRS
+#define CS_REWARD_PAIRS 0
+#endif
+template <class G>
+struct RewardPairs {
+    static constexpr bool value = CS_REWARD_PAIRS && G::P == 2;
+};
+template <int P>
+__device__ __forceinline__ void emit_reward_pairs(float* reward, int64_t rowbase, const float (&r)[P],
+                                                  const LaneCtx& c)
+{
+    const uint32_t a0 = __float_as_uint(r[0]), a1 = __float_as_uint(r[P > 1 ? 1 : 0]);
+    const uint32_t b0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a0, 0x101, 0xF, 0xF, true);   // row_shl:1
+    const uint32_t b1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a1, 0x101, 0xF, 0xF, true);
+    if ((c.lane & 1) == 0 && c.valid) {
+        float* dst = reward + (rowbase + c.env) * 2;
+        if (c.lane + 1 < c.nvalid) out_store16((uint4*)dst, make_uint4(a0, a1, b0, b1));
+        else out_store((uint64_t*)dst, (uint64_t)a0 | (uint64_t)a1 << 32);
     }
 }
 
@@ -564,13 +595,16 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
                 }
             }
 #ifndef CS_PROF_NO_SMALL
-            emit_reward<G>(reward, row, r);
+            if constexpr (!RewardPairs<G>::value) emit_reward<G>(reward, row, r);
             out_store(done_o + row, (uint8_t)done);
 #endif
             if constexpr (DQ == 0) {
                 if (done) g.reset(m);
             }
         }
+#ifndef CS_PROF_NO_SMALL
+        if constexpr (RewardPairs<G>::value) emit_reward_pairs(reward, rowbase, r, c);
+#endif
         if constexpr (DQ > 0) {
             // a lane ending its game with an empty queue makes every lane with room draw one deal ahead, in lockstep
             if (__ballot(c.valid && done && (q.get(0) & 7u) == 0u)) {
