@@ -71,8 +71,67 @@ __device__ __forceinline__ void tally_card(int c, uint64_t& cnt, uint64_t& sm)
 
 // 7-card category << 20 | five tiebreak ranks, from the tallies of the 7 cards (the board's are shared by both
 // players: tallied once)
+// Branch-free form (the default): the rank-count bit planes come from the four suit masks by a bit-sliced adder
+// (count = a + b + c + d per rank bit), every category's tie-break ranks are computed and the category picks them,
+// so a wave's lanes never diverge on the hand category (the if-chain below executes the union of the categories its
+// lanes hold). Same values. CS_EVAL_BRANCHY=1: the if-chain.
+#ifndef CS_EVAL_BRANCHY
+#define CS_EVAL_BRANCHY 0
+#endif
+// highest set bit of m removed; its rank (31 - clz) in r (0xFFFFFFFF for m = 0, never packed)
+__device__ __forceinline__ uint32_t pop_top(uint32_t m, uint32_t& r)
+{
+    const uint32_t z = __clz(m);
+    r = 31u - z;
+    return m & ~(0x80000000u >> (z & 31u));
+}
+__device__ __forceinline__ uint32_t holdem_rank7_bf(uint64_t smp)
+{
+    const uint32_t a = (uint32_t)smp & 0x1FFFu, b = (uint32_t)(smp >> 16) & 0x1FFFu, c = (uint32_t)(smp >> 32) & 0x1FFFu,
+                   d = (uint32_t)(smp >> 48) & 0x1FFFu;
+    const uint32_t x1 = a ^ b, c1 = a & b, x2 = c ^ d, c2 = c & d, c3 = x1 & x2;
+    const uint32_t B0 = x1 ^ x2, B1 = c1 ^ c2 ^ c3, m4 = c1 & c2;           // count = B0 + 2 B1 + 4 m4 per rank
+    const uint32_t m3 = B0 & B1, m2 = B1 & ~B0, m1 = B0 & ~B1, all = a | b | c | d;
+    uint32_t fm = __popc(a) >= 5 ? a : 0u;
+    fm = __popc(b) >= 5 ? b : fm;
+    fm = __popc(c) >= 5 ? c : fm;
+    fm = __popc(d) >= 5 ? d : fm;
+    const int sf = fm ? top_straight13(fm) : -1, st = top_straight13(all);
+    const int n3 = __popc(m3), n2 = __popc(m2);
+    const bool isSF = sf >= 0, isQ = m4 != 0u, isFH = n3 >= 2 || (n3 == 1 && n2 >= 1), isF = fm != 0u,
+               isS = st >= 0, isT = n3 >= 1, is2P = n2 >= 2, isP = n2 >= 1;
+    // the five highest of the flush suit (category flush) or of the single ranks (kickers of trips / pair / high)
+    const bool flush_cat = isF && !isSF && !isQ && !isFH;
+    uint32_t k0, k1, k2, k3, k4;
+    uint32_t x = flush_cat ? fm : m1;
+    x = pop_top(x, k0); x = pop_top(x, k1); x = pop_top(x, k2); x = pop_top(x, k3); (void)pop_top(x, k4);
+    uint32_t q0, t0, p0, p1, rq, rfh, r2p;
+    (void)pop_top(all & ~m4, rq);                    // quads: the kicker is the best other rank
+    const uint32_t r3 = pop_top(m3, t0);
+    (void)pop_top(r3 | m2, rfh);                     // full house: best pair among the other trips and the pairs
+    uint32_t rem2 = pop_top(m2, p0);
+    rem2 = pop_top(rem2, p1);
+    (void)pop_top(all & ~(1u << (p0 & 31u)) & ~(1u << (p1 & 31u)), r2p);   // two pair: best other rank
+    (void)pop_top(m4, q0);
+    uint32_t cat, v;   // v = the five 4-bit tie-break ranks
+    if (isSF) { cat = 9; v = (uint32_t)sf << 16; }
+    else if (isQ) { cat = 8; v = q0 << 16 | rq << 12; }
+    else if (isFH) { cat = 7; v = t0 << 16 | rfh << 12; }
+    else if (isF) { cat = 6; v = k0 << 16 | k1 << 12 | k2 << 8 | k3 << 4 | k4; }
+    else if (isS) { cat = 5; v = (uint32_t)st << 16; }
+    else if (isT) { cat = 4; v = t0 << 16 | k0 << 12 | k1 << 8; }
+    else if (is2P) { cat = 3; v = p0 << 16 | p1 << 12 | r2p << 8; }
+    else if (isP) { cat = 2; v = p0 << 16 | k0 << 12 | k1 << 8 | k2 << 4; }
+    else { cat = 1; v = k0 << 16 | k1 << 12 | k2 << 8 | k3 << 4 | k4; }
+    return cat << 20 | v;
+}
+
 __device__ inline uint32_t holdem_rank7(uint64_t cnt, uint64_t smp)
 {
+    if constexpr (!CS_EVAL_BRANCHY) return holdem_rank7_bf(smp);
+#ifdef CS_PROF_NO_EVAL   // profiling builds only: wrong showdowns, timing of the evaluator
+    return (uint32_t)(cnt ^ (cnt >> 32) ^ smp ^ (smp >> 29)) & 0xFFFFFFu;
+#endif
     const uint32_t sm[4] = {(uint32_t)smp & 0x1FFFu, (uint32_t)(smp >> 16) & 0x1FFFu, (uint32_t)(smp >> 32) & 0x1FFFu,
                             (uint32_t)(smp >> 48) & 0x1FFFu};
     uint32_t m1 = 0, m2 = 0, m3 = 0, m4 = 0;
@@ -161,6 +220,56 @@ __device__ __forceinline__ bool deal9_staged(Rng& rng, uint32_t (&j)[9])
     return true;
 }
 
+// deal9_staged without its 24-step dependency chain. For i = 51..43 (mask 63) a byte u = b & 63 is accepted for every
+// i if u <= 42, for none if u >= 52; only u in 43..51 ("maybe", 9/64 of the bytes) depends on i = 51 - (acceptances
+// before it). SWAR per dword gives the sure-accept and maybe masks of the 24 bytes; the maybes are then resolved in
+// order (a few per lane) from the popcount of the acceptances before each. Same bytes, same draws.
+#ifndef CS_DEAL9_SWAR
+#define CS_DEAL9_SWAR 1
+#endif
+template <class Rng>
+__device__ __forceinline__ bool deal9_swar(Rng& rng, uint32_t (&j)[9])
+{
+    const uint32_t k0 = rng.staged_offset();
+    if (k0 >= rng.sn || rng.sn - k0 < 28u) return false;
+    const uint32_t* row = (const uint32_t*)(rng.stg + (k0 & ~3u));
+    const uint32_t sh = k0 & 3u;
+    uint32_t w[7], x[6];
+#pragma unroll
+    for (int q = 0; q < 7; q++) w[q] = row[q];
+    uint32_t acc = 0, may = 0;
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        x[q] = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh) & 0x3F3F3F3Fu;   // staged bytes k0 + 4q .., & 63
+        const uint32_t ge43 = (x[q] + 0x55555555u) & 0x80808080u, ge52 = (x[q] + 0x4C4C4C4Cu) & 0x80808080u;
+        const uint32_t a = (~ge43 & 0x80808080u) >> 7, m = (ge43 & ~ge52) >> 7;
+        // byte flags (bits 0, 8, 16, 24) -> 4-bit mask: the product's top nibble
+        acc |= ((a * 0x10204080u) >> 28) << (4 * q);
+        may |= ((m * 0x10204080u) >> 28) << (4 * q);
+    }
+    while (may) {
+        const uint32_t t = __builtin_ctz(may);
+        may &= may - 1u;
+        const uint32_t cnt = __popc(acc & ((1u << t) - 1u));
+        if (cnt >= 9u) break;                    // past the ninth draw: not consumed
+        uint32_t d = x[0];
+#pragma unroll
+        for (int q = 1; q < 6; q++) d = (t >> 2) == (uint32_t)q ? x[q] : d;
+        const uint32_t u = (d >> (8u * (t & 3u))) & 63u;
+        acc |= u <= 51u - cnt ? 1u << t : 0u;
+    }
+    if (__popc(acc) < 9) return false;
+    uint32_t p = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        p = __builtin_ctz(acc);
+        acc &= acc - 1u;
+        j[k] = rng.stg[k0 + p] & 63u;
+    }
+    rng.advance_by(p + 1u);
+    return true;
+}
+
 // The hold'em deal (limitholdem/dealer.py: shuffle the 52-card deck, deal_card = pop()) of a heads-up game: hole i ->
 // player i % 2, card i / 2 from deck[51 - i]; flop deck[47..45], turn deck[44], river deck[43]. Fisher-Yates fixes
 // position i at step i, and only deck[43..51] is ever dealt, so the first nine swaps are tracked (swap k writes card vj
@@ -178,7 +287,7 @@ __device__ __forceinline__ void holdem_deal2(Rng& rng, uint32_t& holes, uint32_t
     rng.advance_by(12u);
     staged = true;
 #else
-    if constexpr (Rng::kMode == STAGE_LDS) staged = deal9_staged(rng, js);
+    if constexpr (Rng::kMode == STAGE_LDS) staged = CS_DEAL9_SWAR ? deal9_swar(rng, js) : deal9_staged(rng, js);
 #endif
     if (!staged) {
 #pragma unroll
@@ -186,6 +295,14 @@ __device__ __forceinline__ void holdem_deal2(Rng& rng, uint32_t& holes, uint32_t
     }
     uint32_t JV[9];
     uint32_t d0 = 0, d1 = 0;
+#ifdef CS_PROF_NO_TRACK   // profiling builds only: wrong deals, timing of the swap tracking
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        if (k < 4) d0 |= js[k] << (6 * k);
+        else d1 |= js[k] << (6 * (k - 4));
+    }
+    if (false)
+#endif
 #pragma unroll
     for (int k = 0; k < 9; k++) {
         const uint32_t i = 51 - k, j = js[k];
