@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Benchmark of the env.step hot path (BASELINE.json): env-steps/s (whole node) + achieved HBM GB/s.
 
-One bench "step" = one cs_rollout launch: T fused lockstep env steps (defaults per game in GAMES: Leduc 256, Limit /
-No-limit 128, DouDizhu / Blackjack 64) of the uniform-random legal policy with auto-reset over every env of the
+One bench "step" = one cs_rollout launch: T fused lockstep env steps (defaults per game in GAMES: Leduc, Limit and
+No-limit 256, DouDizhu / Blackjack 64) of the uniform-random legal policy with auto-reset over every env of the
 rank's shard, writing the full trajectory (obs, legal mask, player, action, reward, done) to HBM.
 N>1: one process per GPU (torchrun), rank r owns envs [r*N, (r+1)*N) seeded 42 + global index -- the envs are
 independent, so the timed loop has no data-path collective (weak scaling, `value`). A second timed phase adds the
@@ -36,17 +36,17 @@ MT_N = 624              # words per MT19937 block
 # of 4 blocks, 3 generated at seeding and 3 more per refill once the lane is inside the last one (cs_ring.h:
 # needs_refill at position >= 2 x 624); DouDizhu a two-block word window that twists one block per 624 draws
 # (cs_doudizhu.hip WaveMt::window, first twist ~1 184 draws in).
-# Fused steps per launch, measured on one box: Leduc 256 vs 128 +3 % (T >= 256), Limit / No-limit 128
-# vs 64 +2.5 / +3 %, DouDizhu 128 vs 64 -7 %.
+# Fused steps per launch, measured on one box: Leduc 256 vs 128 +3 % (T >= 256), 512 vs 256 -9 %;
+# Limit / No-limit 256 vs 128 +1.5 / +2 % (128 vs 64 +2.5 / +3 %), DouDizhu 128 vs 64 -7 %.
 RING = dict(first_refill=2 * MT_N, per_refill=3 * MT_N)
 GAMES = {
     'leduc-holdem': dict(envs=1 << 20, T=256, state_bytes=2 * 4 + 4, draws_per_step=2.83, **RING),
-    'limit-holdem': dict(envs=262144, T=128, state_bytes=12 * 4 + 4, draws_per_step=24.5, **RING),
+    'limit-holdem': dict(envs=262144, T=256, state_bytes=12 * 4 + 4, draws_per_step=24.5, **RING),
     'blackjack': dict(envs=1 << 20, T=64, state_bytes=20 * 4 + 4, draws_per_step=57.0, **RING),
     'doudizhu': dict(envs=65536, T=64, state_bytes=20 * 4 + 4, draws_per_step=1.21, first_refill=1184,
                      per_refill=MT_N),
     # not a BASELINE config; draws/step counted on the oracle (4096 envs x 256 random steps)
-    'no-limit-holdem': dict(envs=262144, T=128, state_bytes=4 * 4 + 4, draws_per_step=26.3, **RING),
+    'no-limit-holdem': dict(envs=262144, T=256, state_bytes=4 * 4 + 4, draws_per_step=26.3, **RING),
 }
 TIMED_TARGET_S = 2.0     # default --steps: enough launches for >= ~2 s of timed region (box variance, SMI sampler)
 
