@@ -6,8 +6,8 @@ No-limit 256, DouDizhu / Blackjack 64) of the uniform-random legal policy with a
 rank's shard, writing the full trajectory (obs, legal mask, player, action, reward, done) to HBM.
 N>1: one process per GPU (torchrun), rank r owns envs [r*N, (r+1)*N) seeded 42 + global index -- the envs are
 independent, so the timed loop has no data-path collective (weak scaling, `value`). A second timed phase adds the
-one real exchange, returning the trajectory shards to one place (--gather rank0, the default: point-to-point RCCL
-into rank 0 over xGMI; --gather all: all-gather into every rank), reported under "gather".
+one real exchange, returning the trajectory shards to their consumer: point-to-point RCCL into rank 0 over xGMI
+("gather") and the all-gather into every rank that BASELINE config 5 names ("allgather"); both by default.
 
 A third phase times the same workload with the engine's fast RNG mode (cs_config.rng_mode = CS_RNG_PHILOX: Philox
 byte stream instead of numpy's MT19937, so NOT the reference's deals) and reports it under "rng_philox" -- `value`
@@ -175,8 +175,9 @@ def main():
     ap.add_argument('--game', default='leduc-holdem', choices=sorted(GAMES))
     ap.add_argument('--envs', type=int, default=0, help='envs per GPU (default: the BASELINE config)')
     ap.add_argument('--T', type=int, default=0, help='fused env steps per launch (default: per game, GAMES)')
-    ap.add_argument('--gather', choices=('rank0', 'all', 'none'), default='rank0',
-                    help='N>1: trajectory exchange timed in a second phase (default: every shard into rank 0)')
+    ap.add_argument('--gather', choices=('both', 'rank0', 'all', 'none'), default='both',
+                    help='N>1: trajectory exchange timed after the main loop: every shard into rank 0 ("gather"), '
+                         'all-gathered into every rank (BASELINE config 5, "allgather"), or both (default)')
     ap.add_argument('--gather-steps', type=int, default=5)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-philox', dest='philox', action='store_false',
@@ -187,8 +188,7 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from rlcard_amd.shard import (ShardedVecEnv, gather_traj, gather_traj_to, new_gathered, rank_max, traj_bytes,
-                                  whole_job_rate)
+    from rlcard_amd.shard import ShardedVecEnv, rank_max, time_exchange, whole_job_rate
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -243,29 +243,18 @@ def main():
     elapsed = rank_max(time.perf_counter() - t0, dev)
     kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
 
-    gather_info = None
+    gather_info = {}
     if world > 1 and args.gather != 'none':
-        # the trajectory exchange: rollout + gather per step, timed like the main loop
-        gathered = new_gathered(traj, world) if (args.gather == 'all' or rank == 0) else None
-        torch.cuda.synchronize()
-        barrier()
-        g0 = time.perf_counter()
-        for k in range(args.gather_steps):
-            env.rollout(T, policy_seed=5, t0=t_launch * T, out=traj)
-            t_launch += 1
-            if args.gather == 'all':
-                gather_traj(traj, gathered)
-            else:
-                gather_traj_to(traj, gathered, dst=0)
-        torch.cuda.synchronize()
-        barrier()
-        gel = rank_max(time.perf_counter() - g0, dev)
-        gather_info = dict(mode=args.gather, collective='RCCL %s over xGMI' % (
-                               'all_gather_into_tensor' if args.gather == 'all' else 'send/recv into rank 0'),
-                           steps=args.gather_steps, ms_per_step=1e3 * gel / args.gather_steps,
-                           value=whole_job_rate(N, T, args.gather_steps, gel, world),
-                           bytes_per_rank_per_step=traj_bytes(traj))
-        del gathered
+        # the trajectory exchange: rollout + exchange per step, timed like the main loop
+        for mode in (('rank0', 'all') if args.gather == 'both' else (args.gather,)):
+            def produce():
+                nonlocal t_launch
+                env.rollout(T, policy_seed=5, t0=t_launch * T, out=traj)
+                t_launch += 1
+            info, gathered = time_exchange(produce, traj, mode, args.gather_steps, N, T, torch.cuda.synchronize, dev)
+            gather_info['allgather' if mode == 'all' else 'gather'] = info
+            del gathered
+            torch.cuda.empty_cache()
 
     philox_info = None
     if args.philox and game != 'doudizhu':
@@ -332,8 +321,7 @@ def main():
             else:
                 line['roofline']['traffic'] = tr['bytes_per_launch']
                 line['roofline']['traffic_source'] = tr['source']
-        if gather_info is not None:
-            line['gather'] = gather_info
+        line.update(gather_info)
         if philox_info is not None:
             line['rng_philox'] = philox_info
         if world == 1 and not args.no_cpu_baseline:

@@ -17,7 +17,7 @@ import torch
 import torch.distributed as dist
 
 __all__ = ['shard_range', 'ShardedVecEnv', 'gather_traj', 'gather_traj_to', 'new_gathered', 'rank_max',
-           'whole_job_rate', 'traj_bytes']
+           'whole_job_rate', 'traj_bytes', 'time_exchange']
 
 
 def shard_range(envs_per_rank, rank):
@@ -80,6 +80,35 @@ def rank_max(x, device=None, group=None):
 def whole_job_rate(envs_per_rank, steps_per_launch, launches, elapsed_s, world):
     """env-steps/s of the whole job: every rank's env-steps over the slowest rank's time (weak scaling)."""
     return world * int(envs_per_rank) * int(steps_per_launch) * int(launches) / float(elapsed_s)
+
+
+def time_exchange(produce, traj, mode, steps, envs_per_rank, steps_per_launch, sync=None, device=None):
+    """bench.py's N > 1 exchange phase: `steps` x (produce() refills traj, then the exchange: mode 'rank0' =
+    gather_traj_to rank 0, 'all' = gather_traj into every rank), bracketed by sync() + barrier, timed as the max
+    over ranks. -> (info dict, gathered buffers on the ranks that hold them, else None)."""
+    world = dist.get_world_size()
+    rank = dist.get_rank()
+    gathered = new_gathered(traj, world) if (mode == 'all' or rank == 0) else None
+    sync = sync or (lambda: None)
+    sync()
+    dist.barrier()
+    import time
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        produce()
+        if mode == 'all':
+            gather_traj(traj, gathered)
+        else:
+            gather_traj_to(traj, gathered, dst=0)
+    sync()
+    dist.barrier()
+    el = rank_max(time.perf_counter() - t0, device)
+    info = dict(mode=mode, collective='RCCL %s over xGMI' % (
+                    'all_gather_into_tensor' if mode == 'all' else 'send/recv into rank 0'),
+                steps=steps, ms_per_step=1e3 * el / steps,
+                value=whole_job_rate(envs_per_rank, steps_per_launch, steps, el, world),
+                bytes_per_rank_per_step=traj_bytes(traj))
+    return info, gathered
 
 
 class ShardedVecEnv:

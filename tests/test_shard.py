@@ -112,3 +112,51 @@ def test_two_rank_gather_to_rank0_and_timing(oracle, game, n, T):
     for k, v in full.items():
         g = np.concatenate([got[0][k][r] for r in range(world)], axis=1)
         assert np.array_equal(g, v), k
+
+
+def _worker_exchange(rank, world, port, q):
+    """bench.py's exchange phase (shard.time_exchange) in both modes with a CPU producer."""
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from rlcard_amd.shard import time_exchange
+        traj = {'obs': torch.zeros((4, 8, 3), dtype=torch.uint8), 'reward': torch.zeros((4, 8, 2))}
+        calls = [0]
+
+        def produce():
+            calls[0] += 1
+            traj['obs'].fill_(rank * 10 + calls[0])
+            traj['reward'].fill_(float(rank))
+        res = {}
+        for mode in ('rank0', 'all'):
+            info, g = time_exchange(produce, traj, mode, 3, 8, 4)
+            held = None if g is None else {k: v.clone() for k, v in g.items()}
+            res[mode] = (info, held)
+        q.put((rank, calls[0], {m: (i['mode'], i['steps'], i['value'] > 0, i['bytes_per_rank_per_step'],
+                                    None if h is None else (h['obs'][:, 0, 0, 0].tolist(), h['reward'].shape))
+                                for m, (i, h) in res.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_exchange_phase_of_bench():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_exchange, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (c, m)) for r, c, m in [q.get(timeout=240) for _ in range(2)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        calls, m = res[r]
+        assert calls == 6
+        assert m['rank0'][:3] == ('rank0', 3, True) and m['all'][:3] == ('all', 3, True)
+        assert m['rank0'][3] == 4 * 8 * 3 + 4 * 8 * 2 * 4
+        # the last exchange of each mode holds every rank's last shard: rank r's obs = 10 r + call number
+        assert m['all'][4] == ([3 + 3, 13 + 3], (2, 4, 8, 2))
+    assert res[0][1]['rank0'][4] == ([3, 13], (2, 4, 8, 2))
+    assert res[1][1]['rank0'][4] is None
