@@ -74,6 +74,16 @@ hipError_t np_launch_step(const Buffers& b, const int32_t* actions, const cs_ste
 hipError_t np_launch_observe(const Buffers& b, int32_t player, const cs_step_out& o, hipStream_t s);
 hipError_t np_launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
                              const cs_traj_out& o, hipStream_t s);
+// cs_holdem_n10.hip: the same for 7..10 players (Limit / No-limit)
+int np10_game_info(int32_t game, int32_t num_players, cs_game_info* info);
+int64_t np10_stage_bytes(int32_t game, int32_t num_players);
+hipError_t np10_launch_seed(const Buffers& b, const uint32_t* keys_dev, const int32_t* klen_dev, int64_t first,
+                            int64_t count, hipStream_t s);
+hipError_t np10_launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s);
+hipError_t np10_launch_step(const Buffers& b, const int32_t* actions, const cs_step_out& o, hipStream_t s);
+hipError_t np10_launch_observe(const Buffers& b, int32_t player, const cs_step_out& o, hipStream_t s);
+hipError_t np10_launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
+                               const cs_traj_out& o, hipStream_t s);
 inline bool is_holdem_n(const Buffers& b)
 {
     return (b.game == CS_GAME_LEDUC || b.game == CS_GAME_LIMIT || b.game == CS_GAME_NOLIMIT) && b.num_players > 2;

@@ -1,4 +1,4 @@
-// cs_holdem_n.h -- Leduc / Limit / No-limit hold'em with 3..6 players ('game_num_players', envs/env.py:33-39), as
+// cs_holdem_n.h -- Leduc / Limit / No-limit hold'em with 3..10 players (Leduc 3..5) ('game_num_players', envs/env.py:33-39), as
 // lane-per-env lockstep state machines over the shared skeleton (cs_skeleton.h). The heads-up games keep their
 // specialised kernels (cs_leduc.h, cs_limit.h, cs_nolimit.h); these follow the reference's per-player loops directly.
 //
@@ -307,13 +307,13 @@ struct LeducN {
     }
 };
 
-// ---- Limit Texas Hold'em, P = 3..6 ----------------------------------------------------------------------------------
+// ---- Limit Texas Hold'em, P = 3..10 ----------------------------------------------------------------------------------
 // player word: c0:6 c1:6 in:8 (12) raised:6 (20) folded:1 (26)
 // S0: board c0..c4 6 bits each; S1: ptr:4 rc:3 (4) have_raised:3 (7) not_raise_num:4 (10) use_prev:1 (14) over:1 (31)
 // S2: raise_nums 4 x 3 (0..11), prev_raise_nums 4 x 3 (12..23) (the reset obs shows the previous game's, game.py:98)
 template <int NP>
 struct LimitN {
-    static_assert(NP >= 3 && NP <= 6, "limit: 3..6 players");
+    static_assert(NP >= 3 && NP <= 10, "limit: 3..10 players");
     static constexpr int OBS = 72, A = 4, P = NP, LB = 1, WORDS = NP + 3, ACTION_BYTES = 1, NB = 3;
     static constexpr bool RING = true, RAW_OBS = false, PAYOFF_DRAWS = true;
     static constexpr int SCRATCH_WORDS = 0;
@@ -457,13 +457,13 @@ struct LimitN {
     }
 };
 
-// ---- No-limit Texas Hold'em, P = 3..6 -------------------------------------------------------------------------------
+// ---- No-limit Texas Hold'em, P = 3..10 -------------------------------------------------------------------------------
 // player word: c0:6 c1:6 in:8 (12) raised:8 (20) status:2 (28; 0 alive, 1 folded, 2 all-in)
-// S0: board c0..c4 6 bits each; S1: ptr:4 rc:3 (4) not_raise_num:8 (7) not_playing_num:8 (15) dealer:3 (23)
-//     dealer drawn:1 (26) over:1 (31). The stack is chips_for_each - in (not stored).
+// S0: board c0..c4 6 bits each; S1: ptr:4 rc:3 (4) not_raise_num:8 (7) not_playing_num:8 (15) dealer:4 (23)
+//     dealer drawn:1 (27) over:1 (31). The stack is chips_for_each - in (not stored).
 template <int NP>
 struct NolimitN {
-    static_assert(NP >= 3 && NP <= 6, "no-limit: 3..6 players");
+    static_assert(NP >= 3 && NP <= 10, "no-limit: 3..10 players");
     static constexpr int OBS = 54, A = 5, P = NP, LB = 1, WORDS = NP + 2, ACTION_BYTES = 1, NB = 14;
     static constexpr bool RING = true, RAW_OBS = true, PAYOFF_DRAWS = true;
     static constexpr int SCRATCH_WORDS = 0;
@@ -555,7 +555,7 @@ struct NolimitN {
     {
         int dealer;   // randint(0, N) by the first game when configured None, then kept (game.py:62-63)
         if (dealer_cfg >= 0) dealer = dealer_cfg;
-        else if (bf(s1, 26, 1)) dealer = (int)bf(s1, 23, 3);
+        else if (bf(s1, 27, 1)) dealer = (int)bf(s1, 23, 4);
         else dealer = (int)rng.interval((uint32_t)(NP - 1));
         uint32_t d[2 * NP + 5];
         holdem_deal_k<2 * NP + 5>(rng, d);
@@ -569,7 +569,7 @@ struct NolimitN {
         s0 = 0;
 #pragma unroll
         for (int k = 0; k < 5; k++) s0 |= d[2 * NP + k] << (6 * k);
-        s1 = (uint32_t)next_seat<NP>(bb) | (uint32_t)dealer << 23 | 1u << 26;
+        s1 = (uint32_t)next_seat<NP>(bb) | (uint32_t)dealer << 23 | 1u << 27;
     }
 
     template <class Rng>
@@ -609,7 +609,7 @@ struct NolimitN {
         }
         if (NP - nby == 1 && (int)bf(pw.get(last), 20, 8) >= max_raised()) { by |= 1u << last; nby += 1; }
         if (nrn + npn >= NP) {   // round over: pointer dealer + 1 past bypassed players (unless all are), deal
-            int g = next_seat<NP>((int)bf(s1, 23, 3));
+            int g = next_seat<NP>((int)bf(s1, 23, 4));
             if (nby < NP) {
 #pragma unroll
                 for (int k = 0; k < NP; k++)
@@ -626,7 +626,7 @@ struct NolimitN {
         for (int i = 0; i < NP; i++) in_hand += bf(pw.w[i], 28, 2) != FOLDED ? 1 : 0;
         const uint32_t over = in_hand == 1 || r >= 4;
         s1 = (uint32_t)q | (uint32_t)r << 4 | (uint32_t)(nrn & 255) << 7 | (uint32_t)(npn & 255) << 15 |
-             (s1 & (0xFu << 23)) | over << 31;
+             (s1 & (0x1Fu << 23)) | over << 31;
     }
 
     template <class Rng>

@@ -11,7 +11,7 @@
 namespace cs {
 
 constexpr int TBLOCK = 256;
-constexpr int MAXP = 6;   // players per env (3..6-player hold'em, cs_holdem_n.h)
+constexpr int MAXP = 10;   // players per env (3..10-player hold'em, cs_holdem_n.h)
 
 // One lane per env, scanning its T rows backwards. Row (t, e) is a transition of the player who acted at t:
 //   next_t  its next turn in the same game, -1 = the game ended first (next state = final_obs at row end_t), -2 = the

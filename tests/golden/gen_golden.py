@@ -19,7 +19,7 @@ Fixtures written:
                    env_dealer; -1 = dealer drawn by the game).
   blackjack.npz    same for blackjack (+ the config-1 run_random.py trajectory: env seed 42, np.random.seed(42)).
   doudizhu.npz     same for doudizhu (legal ids as CSR, obs padded to 901).
-  leduc_np.npz / limit_np.npz / nolimit_np.npz   the same streams with game_num_players 3..6 (env_np per env;
+  leduc_np.npz / limit_np.npz / nolimit_np.npz   the same streams with game_num_players 3..10 (env_np per env;
                    no-limit also short stacks for side pots). Leduc's obs raises IndexError in the reference when
                    the others' chips pass slot 35 (envs/leducholdem.py:64): such events are recorded with obs_len -1
                    (obs undefined there) and the game continues through Game.step, as Env.step does before it fails.
@@ -264,10 +264,11 @@ def drive_np(env_id, cfgs, seeds, games, stream):
 
 def gen_nplayer():
     specs = [('leduc-holdem', 'leduc_np', 36, 4, [3, 3, 4, 4, 5, 5], [{}] * 6, 40),
-             ('limit-holdem', 'limit_np', 72, 4, [3, 3, 4, 5, 6, 6], [{}] * 6, 30),
-             ('no-limit-holdem', 'nolimit_np', 54, 5, [3, 3, 4, 4, 6, 6, 3, 4, 6],
+             ('limit-holdem', 'limit_np', 72, 4, [3, 3, 4, 5, 6, 6, 8, 10], [{}] * 8, 30),
+             ('no-limit-holdem', 'nolimit_np', 54, 5, [3, 3, 4, 4, 6, 6, 3, 4, 6, 8, 10, 9],
               [{}] * 6 + [{'chips_for_each': 10}, {'chips_for_each': 6, 'dealer_id': 2},
-                          {'chips_for_each': 20, 'dealer_id': 5}], 40)]
+                          {'chips_for_each': 20, 'dealer_id': 5}, {}, {'chips_for_each': 15},
+                          {'chips_for_each': 8, 'dealer_id': 7}], 40)]
     for env_id, name, O, A, nps, extra, games in specs:
         seeds = [11 + 17 * i for i in range(len(nps))]
         cfgs = [dict(e, game_num_players=n) for n, e in zip(nps, extra)]

@@ -1,4 +1,4 @@
-"""3..6-player hold'em ('game_num_players') on the HIP engine vs the reference streams and the CPU oracle, through the
+"""3..10-player hold'em ('game_num_players') on the HIP engine vs the reference streams and the CPU oracle, through the
 C ABI. Needs a GPU. Kernels: rlcard_amd/csrc/cs_holdem_n.h; oracle: oracle/or_leduc.c, or_limit.c, or_nolimit.c,
 or_judger.c; fixtures: tests/golden/*_np.npz (tests/golden/gen_golden.py --only nplayer)."""
 import numpy as np
@@ -13,7 +13,8 @@ pytestmark = pytest.mark.gpu
 FIXTURES = [('leduc-holdem', 'leduc_np'), ('limit-holdem', 'limit_np'), ('no-limit-holdem', 'nolimit_np')]
 CASES = [('leduc-holdem', 3, {}), ('leduc-holdem', 5, {}), ('limit-holdem', 3, {}), ('limit-holdem', 6, {}),
          ('no-limit-holdem', 4, {}), ('no-limit-holdem', 6, {'chips_for_each': 10}),
-         ('no-limit-holdem', 3, {'chips_for_each': 6, 'dealer_id': 2})]
+         ('no-limit-holdem', 3, {'chips_for_each': 6, 'dealer_id': 2}), ('limit-holdem', 10, {}),
+         ('no-limit-holdem', 8, {'chips_for_each': 15}), ('no-limit-holdem', 10, {'dealer_id': 9})]
 
 
 def _np(o):
