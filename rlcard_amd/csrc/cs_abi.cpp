@@ -177,6 +177,7 @@ int cs_reset(cs_handle* h, const cs_step_out* out, void* stream)
     if (r != CS_OK) return r;
     if (h->b.rec.seq) h->b.rec.seqv++;
     hipError_t e = cs::launch_reset(h->b, *out, (hipStream_t)stream);
+    if (e != hipSuccess && h->b.rec.seq) h->b.rec.seqv--;   // nothing published for this call
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_reset");
 }
 
@@ -188,6 +189,7 @@ int cs_step(cs_handle* h, const int32_t* actions, const cs_step_out* out, void* 
     if (r != CS_OK) return r;
     if (h->b.rec.seq) h->b.rec.seqv++;
     hipError_t e = cs::launch_step(h->b, actions, *out, (hipStream_t)stream);
+    if (e != hipSuccess && h->b.rec.seq) h->b.rec.seqv--;   // nothing published for this call
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_step");
 }
 
@@ -199,6 +201,7 @@ int cs_observe(cs_handle* h, int32_t player, const cs_step_out* out, void* strea
     if (r != CS_OK) return r;
     if (h->b.rec.seq) h->b.rec.seqv++;
     hipError_t e = cs::launch_observe(h->b, player, *out, (hipStream_t)stream);
+    if (e != hipSuccess && h->b.rec.seq) h->b.rec.seqv--;   // nothing published for this call
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_observe");
 }
 
