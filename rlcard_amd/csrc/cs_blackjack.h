@@ -10,18 +10,21 @@
 //   rlcard/games/blackjack/game.py:160-205  state: own hand; dealer hand[1:] until the game is over; is_over
 //   rlcard/games/blackjack/judger.py:2-73   scores with soft aces; winner codes 2 / 1 / -1
 //   rlcard/envs/blackjack.py:38-103         obs = [score(own), score(dealer visible)], legal {hit, stand}, payoff 1/0/-1
-// The deck (52 bytes) and the hands stay in HBM between calls; inside a kernel they live in a per-lane LDS scratch
-// (lane-interleaved words, so uniform word indices are bank-conflict free) because dealing indexes them dynamically.
-// "deck.pop(idx)" is an order-statistic removal: a 52-bit removed mask over the shuffled positions; the idx-th
-// remaining card is the idx-th clear bit.
 // The shuffle is not applied to a deck in memory (51 dependent LDS byte swaps per game were the kernel's critical
 // path): its draws are kept, and the card at a final deck position is found by undoing the swaps from the last one
-// back (~5 vector ops per swap, in registers) -- only the ~6 positions a game deals are ever looked up.
+// back -- only the ~6 positions a game deals are ever looked up. The draws live in registers (13 words); the deal of
+// init_game first draws all of its 2 (P + 1) positions (they depend on the stream and the removed set only) and then
+// traces them back together, four positions per word (SWAR byte compares, ~3 ops per position and swap instead of 5).
+// "deck.pop(idx)" is an order-statistic removal: a 52-bit removed mask over the shuffled positions; the idx-th
+// remaining card is the idx-th clear bit.
 // Packed state, 32 u32 words per env (word-major [32][N]):
 //   0..12  the shuffle's draws: byte k = j of Fisher-Yates swap k (positions 51 - k and j); card id = sorted position
 //   13     removed mask bits 0..31;  14: removed bits 32..51 | deck_len << 20 | game_pointer << 26 | over << 29
-//   15..29 hands: hand h (players 0..P-1, dealer = P) bytes 12h .. 12h+11
+//   15..29 hands: hand h (players 0..P-1, dealer = P) bytes 12h .. 12h+11 (words past 15 + 3 (P + 1) stay zero)
 //   30     hand sizes 4 bits each (5 hands) | winner codes 2 bits per player << 20 (0 none, 1 tie, 2 win, 3 loss)
+// Inside a kernel words 0..12 are registers; 13, 14, 30 and the hands a per-lane LDS scratch (lane-interleaved, so
+// uniform word indices are bank-conflict free; the hands are indexed dynamically), which the reset's draw pass also
+// uses to collect the 51 draws (per-lane byte positions) before they move to registers.
 #pragma once
 #include "cs_device.h"
 
@@ -37,6 +40,12 @@
 #ifndef CS_BJ_RESTAGE_B
 #define CS_BJ_RESTAGE_B 8   // measured with 128-byte rows: 8 > 4 > 1
 #endif
+#ifndef CS_BJ_MIN_WAVES
+#define CS_BJ_MIN_WAVES 3   // the LDS (stage rows + scratch) allows 3 blocks of 4 waves per CU
+#endif
+#ifndef CS_BJ_SWAR_DEAL
+#define CS_BJ_SWAR_DEAL 1   // 0: the initial deal traces its positions one at a time (A/B knob, same cards)
+#endif
 
 namespace cs {
 
@@ -46,24 +55,34 @@ struct Blackjack {
     static constexpr int NB = 1;               // raw obs dwords
     static constexpr bool RING = true;          // MT stream as the byte ring (cs_ring.h)
     static constexpr bool RAW_OBS = true;      // observe() returns byte values, not a 0/1 bitmap
-    static constexpr int SCRATCH_WORDS = WORDS;
+    static constexpr int HAND_CAP = 12;
+    static constexpr int HAND_W = 3 * (NP + 1);                 // state words 15.. the hands use
+    static constexpr int SCRATCH_WORDS = 3 + HAND_W > 13 ? 3 + HAND_W : 13;   // >= 13: the reset's draw bytes
     // MT staging (see MtLaneT)
     static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = CS_BJ_STAGE_W, STAGE_PAD = 8, STAGE_R = CS_BJ_STAGE_R;
     static constexpr int RESTAGE_B = CS_BJ_RESTAGE_B;  // row loads in flight per lane and restage pass
-    static constexpr int MIN_WAVES = 1;  // LDS bounds the occupancy anyway
+    static constexpr int MIN_WAVES = CS_BJ_MIN_WAVES;
     static constexpr int EPW = 64;        // rollout envs per wave (lane_ctx)
     static constexpr int REFILL_K = 2;   // stale blocks twisted per pass (see mt_refill_wave)
-    static constexpr int HAND_CAP = 12;
 
-    uint32_t* s;   // lane scratch: word i at s[i * WAVE]
+    uint32_t* s;       // lane scratch: word i at s[i * WAVE]: 0 = state word 13, 1 = 14, 2 = 30, 3 + q = 15 + q
     int infinite;
+    uint32_t jw[13];   // state words 0..12: the shuffle's draws
 
-    __device__ __forceinline__ uint32_t& W(int i) const { return s[i * WAVE]; }
-    __device__ __forceinline__ int byte_at(int word0, int k) const { return (W(word0 + (k >> 2)) >> (8 * (k & 3))) & 255; }
-    __device__ __forceinline__ void set_byte(int word0, int k, int v) const
+    __device__ __forceinline__ uint32_t& L(int i) const { return s[i * WAVE]; }
+    __device__ __forceinline__ uint32_t& removed_lo() const { return L(0); }
+    __device__ __forceinline__ uint32_t& meta() const { return L(1); }     // state word 14
+    __device__ __forceinline__ uint32_t& sizes() const { return L(2); }    // state word 30
+    __device__ __forceinline__ int hand_byte(int h, int k) const
     {
-        uint32_t& w = W(word0 + (k >> 2));
-        const int sh = 8 * (k & 3);
+        const int b = HAND_CAP * h + k;
+        return (L(3 + (b >> 2)) >> (8 * (b & 3))) & 255;
+    }
+    __device__ __forceinline__ void set_hand_byte(int h, int k, int v) const
+    {
+        const int b = HAND_CAP * h + k;
+        uint32_t& w = L(3 + (b >> 2));
+        const int sh = 8 * (b & 3);
         w = (w & ~(255u << sh)) | ((uint32_t)v << sh);
     }
 
@@ -75,24 +94,44 @@ struct Blackjack {
     __device__ __forceinline__ void load(const uint32_t* st, int64_t n, int64_t env)
     {
 #pragma unroll
-        for (int i = 0; i < WORDS; i++) W(i) = st[(int64_t)i * n + env];
+        for (int i = 0; i < 13; i++) jw[i] = st[(int64_t)i * n + env];
+        removed_lo() = st[13 * n + env];
+        meta() = st[14 * n + env];
+        sizes() = st[30 * n + env];
+#pragma unroll
+        for (int q = 0; q < HAND_W; q++) L(3 + q) = st[(int64_t)(15 + q) * n + env];
     }
     __device__ __forceinline__ void store(uint32_t* st, int64_t n, int64_t env) const
     {
 #pragma unroll
-        for (int i = 0; i < WORDS; i++) st[(int64_t)i * n + env] = W(i);
+        for (int i = 0; i < 13; i++) st[(int64_t)i * n + env] = jw[i];
+        st[13 * n + env] = removed_lo();
+        st[14 * n + env] = meta();
+        st[30 * n + env] = sizes();
+#pragma unroll
+        for (int q = 0; q < 15; q++) st[(int64_t)(15 + q) * n + env] = q < HAND_W ? L(3 + q) : 0u;
+        st[31 * n + env] = 0u;
+    }
+    __device__ __forceinline__ void clear_table() const
+    {
+        removed_lo() = 0;
+        meta() = 52u << 20;
+        sizes() = 0;
+#pragma unroll
+        for (int q = 0; q < HAND_W; q++) L(3 + q) = 0;
     }
     __device__ __forceinline__ void blank()
     {
 #pragma unroll
-        for (int i = 0; i < WORDS; i++) W(i) = 0;
-        W(14) = 1u << 29;
+        for (int i = 0; i < 13; i++) jw[i] = 0;
+        clear_table();
+        meta() = 1u << 29;
     }
 
-    __device__ __forceinline__ int nhand(int h) const { return (W(30) >> (4 * h)) & 15; }
-    __device__ __forceinline__ int winner(int p) const { return (W(30) >> (20 + 2 * p)) & 3; }
-    __device__ __forceinline__ int current() const { return (W(14) >> 26) & 7; }
-    __device__ __forceinline__ bool is_over() const { return (W(14) >> 29) & 1; }
+    __device__ __forceinline__ int nhand(int h) const { return (sizes() >> (4 * h)) & 15; }
+    __device__ __forceinline__ int winner(int p) const { return (sizes() >> (20 + 2 * p)) & 3; }
+    __device__ __forceinline__ int current() const { return (meta() >> 26) & 7; }
+    __device__ __forceinline__ bool is_over() const { return (meta() >> 29) & 1; }
     __device__ __forceinline__ uint32_t legal() const { return 3u; }
 
     __device__ static __forceinline__ int card_value(int c)
@@ -106,7 +145,7 @@ struct Blackjack {
         int sc = 0, aces = 0;
         const int n = nhand(h);
         for (int k = from; k < n; k++) {
-            const int c = byte_at(15, HAND_CAP * h + k);
+            const int c = hand_byte(h, k);
             sc += card_value(c);
             aces += (c % 13) == 0;
         }
@@ -136,36 +175,62 @@ struct Blackjack {
     // the card at final deck position x: undo the swaps from the last (i = 1) to the first (i = 51)
     __device__ __forceinline__ int card_at(int x) const
     {
-        uint32_t jw[13];
-#pragma unroll
-        for (int w = 0; w < 13; w++) jw[w] = W(w);
 #pragma unroll
         for (int i = 1; i <= 51; i++) {
             const int k = 51 - i;
-            const int j = (int)((jw[k >> 2] >> (8 * (k & 3))) & 255u);
+            const int j = (int)__builtin_amdgcn_ubfe(jw[k >> 2], 8 * (k & 3), 6);
             x = x == i ? j : (x == j ? i : x);
         }
         return x;
     }
+    // card_at for four positions per word (bytes; unused bytes 63 never match): undoing swap (i, j) flips a byte
+    // x in {i, j} by i ^ j. Bytes are < 64, so (b + 0x7F) sets bit 7 exactly when b != 0, without carries.
+    template <int NW>
+    __device__ __forceinline__ void cards_at(uint32_t (&X)[NW]) const
+    {
+#pragma unroll
+        for (int i = 1; i <= 51; i++) {
+            const int k = 51 - i;
+            const uint32_t J = __builtin_amdgcn_perm(0u, jw[k >> 2], (uint32_t)(k & 3) * 0x01010101u);   // j x 4
+            const uint32_t I = (uint32_t)i * 0x01010101u, D = I ^ J;
+#pragma unroll
+            for (int w = 0; w < NW; w++) {
+                const uint32_t both = ((X[w] ^ I) + 0x7F7F7F7Fu) & ((X[w] ^ J) + 0x7F7F7F7Fu);
+                const uint32_t m = ~both & 0x80808080u;
+                X[w] ^= D & (m - (m >> 7));
+            }
+        }
+    }
 
+    // Dealer.deal_card's draw: idx = choice(len(deck)), the idx-th remaining position; deck.pop(idx) unless infinite
+    template <class Rng>
+    __device__ __forceinline__ int deal_pos(Rng& rng)
+    {
+        const uint32_t m1 = meta();
+        const int len = (m1 >> 20) & 63;
+        const int idx = (int)rng.interval((uint32_t)(len - 1));
+        const uint64_t avail = ~((uint64_t)removed_lo() | (uint64_t)(m1 & 0xFFFFFu) << 32) & ((1ull << 52) - 1);
+        const int pos = select_bit(avail, idx);
+        if (!infinite) {
+            uint32_t m2 = (m1 & ~(63u << 20)) | (uint32_t)(len - 1) << 20;
+            if (pos < 32) removed_lo() |= 1u << pos;
+            else m2 |= 1u << (pos - 32);
+            meta() = m2;
+        }
+        return pos;
+    }
+    __device__ __forceinline__ void add_card(int h, int c)
+    {
+        const int n = nhand(h);
+        if (n < HAND_CAP) {      // 12 cards always bust a 1-deck hand before this bound
+            set_hand_byte(h, n, c);
+            sizes() += 1u << (4 * h);
+        }
+    }
     template <class Rng>
     __device__ __forceinline__ void deal(Rng& rng, int h)
     {
-        const int len = (W(14) >> 20) & 63;
-        const int idx = (int)rng.interval((uint32_t)(len - 1));
-        const uint64_t avail = ~((uint64_t)W(13) | (uint64_t)(W(14) & 0xFFFFFu) << 32) & ((1ull << 52) - 1);
-        const int pos = select_bit(avail, idx);
-        const int c = card_at(pos);
-        if (!infinite) {
-            if (pos < 32) W(13) |= 1u << pos;
-            else W(14) |= 1u << (pos - 32);
-            W(14) = (W(14) & ~(63u << 20)) | ((uint32_t)(len - 1) << 20);
-        }
-        const int n = nhand(h);
-        if (n < HAND_CAP) {      // 12 cards always bust a 1-deck hand before this bound
-            set_byte(15, HAND_CAP * h + n, c);
-            W(30) += 1u << (4 * h);
-        }
+        add_card(h, card_at(deal_pos(rng)));
     }
 
     __device__ __forceinline__ void observe(int player, uint32_t (&raw)[NB]) const
@@ -178,17 +243,30 @@ struct Blackjack {
     template <class Rng>
     __device__ __forceinline__ void reset(Rng& rng)
     {
-        // 52-card Fisher-Yates (i = 51..1, j = randint(0, i + 1)): its draws, byte k of words 0..12 (LDS byte stores),
-        // then the initial deal
+        // 52-card Fisher-Yates (i = 51..1, j = randint(0, i + 1)): its draws, byte k of scratch words 0..12 (LDS byte
+        // stores at per-lane positions), then into registers; then the initial deal (game.py:22-54): two rounds of
+        // players 0..P-1 and the dealer
         uint8_t* jb = (uint8_t*)s;
         rng.draw_intervals(51u, [&](uint32_t k, uint32_t j) { jb[(k >> 2) * (WAVE * 4) + (k & 3u)] = (uint8_t)j; });
-        W(13) = 0;
-        W(14) = 52u << 20;
 #pragma unroll
-        for (int w = 15; w <= 30; w++) W(w) = 0;
-        for (int r = 0; r < 2; r++) {
-            for (int j = 0; j < NP; j++) deal(rng, j);
-            deal(rng, NP);
+        for (int w = 0; w < 13; w++) jw[w] = L(w);
+        jw[12] &= 0xFFFFFFu;   // byte 51: no draw
+        clear_table();
+        constexpr int ND = 2 * (NP + 1), NW = (ND + 3) / 4;
+        if constexpr (CS_BJ_SWAR_DEAL) {
+            uint32_t X[NW];
+#pragma unroll
+            for (int w = 0; w < NW; w++) X[w] = 0x3F3F3F3Fu;
+#pragma unroll
+            for (int d = 0; d < ND; d++) {
+                const uint32_t sh = 8u * (uint32_t)(d & 3);
+                X[d >> 2] = (X[d >> 2] & ~(255u << sh)) | (uint32_t)deal_pos(rng) << sh;
+            }
+            cards_at(X);
+#pragma unroll
+            for (int d = 0; d < ND; d++) add_card(d % (NP + 1), (int)((X[d >> 2] >> (8 * (d & 3))) & 255u));
+        } else {
+            for (int d = 0; d < ND; d++) deal(rng, d % (NP + 1));
         }
     }
 
@@ -208,8 +286,8 @@ struct Blackjack {
             else code = 1;
             win |= (uint32_t)code << (20 + 2 * p);
         }
-        W(30) = (W(30) & 0xFFFFFu) | win;
-        W(14) = (W(14) & ~(7u << 26)) | 1u << 29;   // game_pointer = 0, over
+        sizes() = (sizes() & 0xFFFFFu) | win;
+        meta() = (meta() & ~(7u << 26)) | 1u << 29;   // game_pointer = 0, over
     }
 
     template <class Rng>
@@ -223,7 +301,7 @@ struct Blackjack {
         }
         if (advance) {
             if (gp >= NP - 1) finish(rng);
-            else W(14) = (W(14) & ~(7u << 26)) | (uint32_t)(gp + 1) << 26;
+            else meta() = (meta() & ~(7u << 26)) | (uint32_t)(gp + 1) << 26;
         }
     }
 
