@@ -68,6 +68,9 @@ struct Blackjack {
     uint32_t* s;       // lane scratch: word i at s[i * WAVE]: 0 = state word 13, 1 = 14, 2 = 30, 3 + q = 15 + q
     int infinite;
     uint32_t jw[13];   // state words 0..12: the shuffle's draws
+    // running judge totals (registers, rebuilt from the hands by load()): hand h's card values with aces as 11 |
+    // its aces << 8; [NP + 1] the same over the dealer's cards after the first (the visible dealer score)
+    uint32_t tot[NP + 2];
 
     __device__ __forceinline__ uint32_t& L(int i) const { return s[i * WAVE]; }
     __device__ __forceinline__ uint32_t& removed_lo() const { return L(0); }
@@ -100,6 +103,17 @@ struct Blackjack {
         sizes() = st[30 * n + env];
 #pragma unroll
         for (int q = 0; q < HAND_W; q++) L(3 + q) = st[(int64_t)(15 + q) * n + env];
+#pragma unroll
+        for (int h = 0; h <= NP; h++) {
+            uint32_t t = 0, t1 = 0;
+            for (int k = 0; k < nhand(h); k++) {
+                const uint32_t v = card_tot(hand_byte(h, k));
+                t += v;
+                t1 += k > 0 ? v : 0u;
+            }
+            tot[h] = t;
+            if (h == NP) tot[NP + 1] = t1;
+        }
     }
     __device__ __forceinline__ void store(uint32_t* st, int64_t n, int64_t env) const
     {
@@ -112,13 +126,15 @@ struct Blackjack {
         for (int q = 0; q < 15; q++) st[(int64_t)(15 + q) * n + env] = q < HAND_W ? L(3 + q) : 0u;
         st[31 * n + env] = 0u;
     }
-    __device__ __forceinline__ void clear_table() const
+    __device__ __forceinline__ void clear_table()
     {
         removed_lo() = 0;
         meta() = 52u << 20;
         sizes() = 0;
 #pragma unroll
         for (int q = 0; q < HAND_W; q++) L(3 + q) = 0;
+#pragma unroll
+        for (int h = 0; h < NP + 2; h++) tot[h] = 0;
     }
     __device__ __forceinline__ void blank()
     {
@@ -139,18 +155,27 @@ struct Blackjack {
         const int r = c % 13;
         return r == 0 ? 11 : (r >= 9 ? 10 : r + 1);
     }
-    // judge_score over cards [from, n) of hand h
+    // a card's judge value (judger.py judge_score: A = 11, J/Q/K = 10) | ace << 8
+    __device__ static __forceinline__ uint32_t card_tot(int c)
+    {
+        const int r = c % 13;
+        return r == 0 ? 11u + 256u : (r >= 9 ? 10u : (uint32_t)r + 1u);
+    }
+    // judge_score from a running total: aces count 1 instead of 11 while the score is over 21, i.e.
+    // min(aces, ceil((score - 21) / 10)) of them ((x * 205) >> 11 == x / 10 for the x <= 132 here)
+    __device__ static __forceinline__ int score_of(uint32_t t)
+    {
+        const int sc = (int)(t & 255u), aces = (int)(t >> 8);
+        const int need = sc > 21 ? ((sc - 12) * 205) >> 11 : 0;
+        return sc - 10 * (need < aces ? need : aces);
+    }
+    // judge_score of hand h (all its cards; from = 1: the dealer's cards after the first)
     __device__ __forceinline__ int score(int h, int from) const
     {
-        int sc = 0, aces = 0;
-        const int n = nhand(h);
-        for (int k = from; k < n; k++) {
-            const int c = hand_byte(h, k);
-            sc += card_value(c);
-            aces += (c % 13) == 0;
-        }
-        while (sc > 21 && aces > 0) { aces--; sc -= 10; }
-        return sc;
+        uint32_t t = tot[0];
+#pragma unroll
+        for (int q = 1; q <= NP; q++) t = h == q ? tot[q] : t;
+        return score_of(from ? tot[NP + 1] : t);
     }
 
     // the k-th (0-based) set bit of a 64-bit mask: popcount bisection, no per-bit loop
@@ -175,10 +200,21 @@ struct Blackjack {
     // the card at final deck position x: undo the swaps from the last (i = 1) to the first (i = 51)
     __device__ __forceinline__ int card_at(int x) const
     {
+#ifdef CS_PROF_BJ_NOTRACE   // profiling builds only: wrong cards, timing of the swap trace-back
+        return x;
+#endif
+        // the draws pass through an empty asm: opaque values, so the compiler cannot hoist the 51 extracted draws out
+        // of the dealer's loop into 51 live registers (occupancy)
+        uint32_t w[13];
+#pragma unroll
+        for (int q = 0; q < 13; q++) {
+            w[q] = jw[q];
+            asm volatile("" : "+v"(w[q]));
+        }
 #pragma unroll
         for (int i = 1; i <= 51; i++) {
             const int k = 51 - i;
-            const int j = (int)__builtin_amdgcn_ubfe(jw[k >> 2], 8 * (k & 3), 6);
+            const int j = (int)__builtin_amdgcn_ubfe(w[k >> 2], 8 * (k & 3), 6);
             x = x == i ? j : (x == j ? i : x);
         }
         return x;
@@ -188,6 +224,9 @@ struct Blackjack {
     template <int NW>
     __device__ __forceinline__ void cards_at(uint32_t (&X)[NW]) const
     {
+#ifdef CS_PROF_BJ_NOTRACE
+        return;
+#endif
 #pragma unroll
         for (int i = 1; i <= 51; i++) {
             const int k = 51 - i;
@@ -225,6 +264,10 @@ struct Blackjack {
         if (n < HAND_CAP) {      // 12 cards always bust a 1-deck hand before this bound
             set_hand_byte(h, n, c);
             sizes() += 1u << (4 * h);
+            const uint32_t v = card_tot(c);
+#pragma unroll
+            for (int q = 0; q <= NP; q++) tot[q] += h == q ? v : 0u;
+            tot[NP + 1] += h == NP && n > 0 ? v : 0u;
         }
     }
     template <class Rng>
