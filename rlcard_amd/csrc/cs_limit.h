@@ -270,6 +270,9 @@ __device__ __forceinline__ bool deal9_swar(Rng& rng, uint32_t (&j)[9])
     return true;
 }
 
+#ifndef CS_TRACK_SWAR
+#define CS_TRACK_SWAR 1   // 0: the JV table (per-swap position / card pairs looked up by the later swaps)
+#endif
 // The hold'em deal (limitholdem/dealer.py: shuffle the 52-card deck, deal_card = pop()) of a heads-up game: hole i ->
 // player i % 2, card i / 2 from deck[51 - i]; flop deck[47..45], turn deck[44], river deck[43]. Fisher-Yates fixes
 // position i at step i, and only deck[43..51] is ever dealt, so the first nine swaps are tracked (swap k writes card vj
@@ -295,6 +298,36 @@ __device__ __forceinline__ void holdem_deal2(Rng& rng, uint32_t& holes, uint32_t
     }
     uint32_t JV[9];
     uint32_t d0 = 0, d1 = 0;
+#if CS_TRACK_SWAR && !defined(CS_PROF_NO_TRACK)
+    // Dealt card k is the card at position 51 - k after the nine swaps (later swaps never touch positions >= 43): the
+    // nine positions, four per word (bytes; 63 = unused, never matches), are traced back through the swaps q = 8 .. 0
+    // -- a byte x in {i_q, j_q} flips by i_q ^ j_q; bytes < 64, so (b + 0x7F) sets bit 7 exactly when b != 0 -- and end
+    // at their initial positions = the card ids. Six live words instead of the JV table's ~40 registers.
+    uint32_t X[3] = {0x30313233u, 0x2C2D2E2Fu, 0x3F3F3F2Bu};   // byte b of X[w]: position 51 - (4 w + b)
+#pragma unroll
+    for (int q = 8; q >= 0; q--) {
+        const uint32_t I = (uint32_t)(51 - q) * 0x01010101u;
+        const uint32_t J = __builtin_amdgcn_perm(0u, js[q], 0u);   // byte 0 of js[q] in every byte
+        const uint32_t D = I ^ J;
+#pragma unroll
+        for (int w = 0; w < 3; w++) {
+            if (q > 4 * w + 3) continue;   // swap q never touches positions 51 - k, k < q (both of its are <= 51 - q)
+            const uint32_t both = ((X[w] ^ I) + 0x7F7F7F7Fu) & ((X[w] ^ J) + 0x7F7F7F7Fu);
+            const uint32_t m = ~both & 0x80808080u;
+            X[w] ^= D & (m - (m >> 7));
+        }
+    }
+    {
+        constexpr int F0[4] = {0, 12, 6, 18};   // hole i -> player i % 2, card i / 2
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            const uint32_t v = (X[k >> 2] >> (8 * (k & 3))) & 63u;
+            if (k < 4) d0 |= v << F0[k < 4 ? k : 0];
+            else d1 |= v << (6 * (k - 4));
+        }
+    }
+    if (false)
+#endif
 #ifdef CS_PROF_NO_TRACK   // profiling builds only: wrong deals, timing of the swap tracking
 #pragma unroll
     for (int k = 0; k < 9; k++) {
@@ -327,6 +360,9 @@ __device__ __forceinline__ void holdem_deal2(Rng& rng, uint32_t& holes, uint32_t
     board = d1;
 }
 
+#ifndef CS_SHOWDOWN_SERIAL
+#define CS_SHOWDOWN_SERIAL 1
+#endif
 // the showdown of a heads-up deal when both players stay in (Judger.judge_game -> compare_hands, judger.py:11-108,
 // utils.py): bit 0 = player 0 wins or ties, bit 1 = player 1. It depends on the deal alone: no-limit evaluates it when
 // the deal is drawn (in the rollout's lockstep deal passes) and keeps it in the state; limit at the game's end.
@@ -340,7 +376,15 @@ __device__ __forceinline__ uint32_t holdem_showdown(uint32_t holes, uint32_t boa
     tally_card((int)((holes >> 6) & 63u), c0, s0);
     tally_card((int)((holes >> 12) & 63u), c1, s1);
     tally_card((int)((holes >> 18) & 63u), c1, s1);
-    const uint32_t v0 = holdem_rank7(c0, s0), v1 = holdem_rank7(c1, s1);
+    uint32_t v0 = holdem_rank7(c0, s0);
+#if CS_SHOWDOWN_SERIAL
+    // the second evaluation's inputs pass through an empty asm with the first result: the two branch-free evaluations
+    // run one after the other instead of interleaved (half the live temporaries: occupancy, no spills)
+    uint32_t s1lo = (uint32_t)s1, s1hi = (uint32_t)(s1 >> 32);
+    asm volatile("" : "+v"(v0), "+v"(s1lo), "+v"(s1hi));
+    s1 = (uint64_t)s1hi << 32 | s1lo;
+#endif
+    const uint32_t v1 = holdem_rank7(c1, s1);
     return (uint32_t)(v0 >= v1) | (uint32_t)(v1 >= v0) << 1;
 }
 
