@@ -70,8 +70,46 @@ def report(d):
     return res
 
 
+def ceiling():
+    """Achievable HBM rates of plain streams (the practical ceiling beside the 8 TB/s spec): the calibration kernels
+    timed with HIP events on the null stream (they launch there; each call also synchronizes), 2 GiB per dispatch, plus torch's fill_."""
+    import torch
+    L = C.CDLL(os.path.join(HERE, 'libcalib.so'))
+    L.calib_read16.argtypes = [C.c_void_p, C.c_int64, C.c_void_p]
+    for f in ('calib_write16', 'calib_write4', 'calib_write1'):
+        getattr(L, f).argtypes = [C.c_void_p, C.c_int64, C.c_int]
+    dev = torch.device('cuda', 0)
+    a = torch.zeros(2 * GIB + 4096, dtype=torch.uint8, device=dev)
+    out = torch.zeros(4, dtype=torch.int32, device=dev)
+    P = lambda t: C.c_void_p(t.data_ptr())
+    cases = [('read16', lambda: L.calib_read16(P(a), 2 * GIB, P(out))),
+             ('write16', lambda: L.calib_write16(P(a), 2 * GIB, 0)),
+             ('write16nt', lambda: L.calib_write16(P(a), 2 * GIB, 1)),
+             ('write4', lambda: L.calib_write4(P(a), 2 * GIB, 0)),
+             ('write4nt', lambda: L.calib_write4(P(a), 2 * GIB, 1)),
+             ('write1', lambda: L.calib_write1(P(a), 2 * GIB, 0)),
+             ('write1nt', lambda: L.calib_write1(P(a), 2 * GIB, 1)),
+             ('torch_fill', lambda: a[:2 * GIB].fill_(7))]
+    res = {}
+    for name, f in cases:
+        for _ in range(3):
+            f()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            f()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 20
+        res[name] = {'ms': ms, 'GB/s': 2 * GIB / ms / 1e6}
+    print(json.dumps(res, indent=1))
+
+
 if __name__ == '__main__':
-    if len(sys.argv) > 2 and sys.argv[1] == '--report':
+    if len(sys.argv) > 1 and sys.argv[1] == '--ceiling':
+        ceiling()
+    elif len(sys.argv) > 2 and sys.argv[1] == '--report':
         report(sys.argv[2])
     else:
         run()
