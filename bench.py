@@ -257,7 +257,7 @@ def main():
             torch.cuda.empty_cache()
 
     philox_info = None
-    if args.philox and game != 'doudizhu':
+    if args.philox:
         # the engine's fast RNG mode on the same workload (not the reference's deals): own envs, same buffers
         del env
         penv = ShardedVecEnv(game, N, rank, seed=42, device=local, config={'rng_mode': 'philox'})

@@ -42,7 +42,7 @@ typedef struct {
     int32_t rng_mode;       /* CS_RNG_MT19937 (0): every env draws numpy's RandomState stream of its seed, bit-exact
                                with the reference; CS_RNG_PHILOX (1): a counter-based Philox4x32-10 byte stream keyed
                                by the same seed key -- same games and rules, NOT the reference's deals; no MT19937
-                               state traffic (lane-per-env games; doudizhu: unsupported) */
+                               state traffic (every game; doudizhu draws the same byte stream) */
     int32_t reserved[3];
 } cs_config;
 

@@ -68,8 +68,6 @@ int cs_create(cs_handle** out, int32_t game, int64_t num_envs, int32_t device, c
     if (num_envs <= 0) return fail(CS_E_INVALID, "num_envs must be positive");
     if (cfg && cfg->rng_mode != CS_RNG_MT19937 && cfg->rng_mode != CS_RNG_PHILOX)
         return fail(CS_E_INVALID, "rng_mode must be CS_RNG_MT19937 or CS_RNG_PHILOX");
-    if (cfg && cfg->rng_mode == CS_RNG_PHILOX && game == CS_GAME_DOUDIZHU)
-        return fail(CS_E_UNSUPPORTED, "CS_RNG_PHILOX: lane-per-env games only (doudizhu keeps MT19937)");
     cs_game_info info;
     int r = cs_game_info_get(game, cfg, &info);
     if (r != CS_OK) return r;

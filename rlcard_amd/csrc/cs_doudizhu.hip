@@ -234,15 +234,32 @@ __device__ __forceinline__ uint32_t decode_action(int32_t a, const Env& e, const
 }
 
 // ---- MT19937 stream of this env, read by the whole wave --------------------------------------------------------
+// Philox mode (cs_config.rng_mode = CS_RNG_PHILOX, ctl bit 18; not the reference's deals): draw k is byte k % 16 of
+// Philox4x32-10(key = the env's init_by_array key, counter = (k / 624, (k % 624) / 16)) -- the lane-per-env games'
+// Philox byte stream (cs_ring.h), so every rule and the oracle's restatement (oracle/or_rng.c) are shared. The draws
+// only use the low 6 bits (interval(i <= 53)). The env's word buffer then holds the key (words 0, 1) and the absolute
+// draw count (word 2); `pos` still counts draws modulo 1 248 (the host's rng_position).
+// The mode is a template parameter (the kernels are instantiated for both), so the MT19937 path carries no Philox code.
+constexpr uint32_t CTL_PHX = 1u << 18;
+template <bool PHX>
 struct WaveMt {
     uint32_t* base;
     uint32_t pos, stale;
+    uint32_t dabs;   // Philox mode: the absolute draw count
+    uint64_t key;
     // 64 tempered words from pos (lane k: word pos + k); twists the next block first if the window reaches it or
     // ends exactly at its start: advance() never moves past the window, so a later crossing into the next block
     // always finds it twisted (with `>` a window ending on the block edge left the next block stale -- the first
     // deal after such a crossing read the block consumed 1 248 draws earlier; tests/test_gpu_refill.py)
     __device__ __forceinline__ uint32_t window(int lane)
     {
+        if constexpr (PHX) {
+            const uint32_t k = dabs + (uint32_t)lane, b = k % 16u;
+            uint32_t w[4];
+            philox4(key, (uint64_t)(k / (uint32_t)MT_N), (uint64_t)((k % (uint32_t)MT_N) / 16u), w);
+            const uint32_t q = b >> 2, word = q == 0 ? w[0] : (q == 1 ? w[1] : (q == 2 ? w[2] : w[3]));
+            return (word >> (8u * (b & 3u))) & 255u;
+        }
         const uint32_t end = pos < (uint32_t)MT_N ? (uint32_t)MT_N : (uint32_t)MT_WORDS;
         if (stale && pos + WAVE >= end) {
             const uint32_t cur = pos < (uint32_t)MT_N ? 0u : (uint32_t)MT_N;
@@ -257,18 +274,26 @@ struct WaveMt {
     }
     __device__ __forceinline__ void advance(uint32_t k)
     {
+        if constexpr (PHX) dabs += k;
         uint32_t np = pos + k;
         const bool crossed = pos < (uint32_t)MT_N ? np >= (uint32_t)MT_N : np >= (uint32_t)MT_WORDS;
         if (np >= (uint32_t)MT_WORDS) np -= MT_WORDS;
         if (crossed) stale = 1;
         pos = np;
     }
+    // the stream position back to ctl (and the Philox draw count to the word buffer); one lane
+    __device__ __forceinline__ void save(uint32_t* ctl, int64_t env) const
+    {
+        ctl[env] = pos | (stale << 16) | (PHX ? CTL_PHX : 0u);
+        if constexpr (PHX) base[2] = dabs;
+    }
 };
 
 // Dealer.shuffle + deal_cards + landlord's 3 cards (dealer.py:12-76; game.py:23-53): np.random.shuffle of the
 // sorted 54-card deck (position k holds rank k / 4, 52 = black joker, 53 = red joker), hands deck[0:17] (landlord),
 // [17:34], [34:51], landlord + deck[51:54]
-__device__ __forceinline__ void deal(Env& e, WaveMt& m, int lane)
+template <class M>
+__device__ __forceinline__ void deal(Env& e, M& m, int lane)
 {
     uint32_t deck = (uint32_t)lane;
     uint32_t win = m.window(lane);
@@ -600,13 +625,20 @@ __device__ __forceinline__ Ctx ctx_of(int64_t n)
     return c;
 }
 
-__device__ __forceinline__ WaveMt wave_mt(uint32_t* mt, const uint32_t* ctl, int64_t env)
+template <bool PHX>
+__device__ __forceinline__ WaveMt<PHX> wave_mt(uint32_t* mt, const uint32_t* ctl, int64_t env)
 {
-    WaveMt m;
+    WaveMt<PHX> m;
     m.base = mt + env * MT_WORDS;
     const uint32_t w = ctl[env];
     m.pos = w & 0x7FFu;
     m.stale = (w >> 16) & 1u;
+    m.dabs = 0;
+    m.key = 0;
+    if constexpr (PHX) {
+        m.key = (uint64_t)m.base[0] | (uint64_t)m.base[1] << 32;
+        m.dabs = m.base[2];
+    }
     return m;
 }
 
@@ -636,6 +668,7 @@ __device__ __forceinline__ void payoffs(const Env& e, float* r)   // judger.py:3
     r[2] = r[1];
 }
 
+template <bool PHX>
 __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
                                                   cs_step_out out, Tab tb, StepRecord rec)
 {
@@ -646,7 +679,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, ui
     if (!c.valid) return;
     WaveLds& L = lds[c.wid];
     Env e;
-    WaveMt m = wave_mt(mt, ctl, c.env);
+    auto m = wave_mt<PHX>(mt, ctl, c.env);
     deal(e, m, c.lane);
     emit_state(e, e.cur, tb, tl, L, c.lane, c.env, out);
     if (c.lane == 0 && out.reward) {
@@ -654,7 +687,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, ui
         r[0] = r[1] = r[2] = 0.f;
     }
     e.store(st, c.env, c.lane);
-    if (c.lane == 0) ctl[c.env] = m.pos | (m.stale << 16);
+    if (c.lane == 0) m.save(ctl, c.env);
     if (rec.seq != nullptr && c.env == rec.env) {   // StepRecord (cs_engine.h): state words, fence, sequence number
         e.store(rec.words, 0, c.lane);
         __threadfence_system();
@@ -662,6 +695,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, ui
     }
 }
 
+template <bool PHX>
 __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
                                                  const int32_t* actions, cs_step_out out, Tab tb, StepRecord rec)
 {
@@ -673,7 +707,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uin
     WaveLds& L = lds[c.wid];
     Env e;
     e.load(st, c.env, c.lane, tb);
-    WaveMt m = wave_mt(mt, ctl, c.env);
+    auto m = wave_mt<PHX>(mt, ctl, c.env);
     float r[3] = {0.f, 0.f, 0.f};
     bool done = false;
     if (e.over()) {
@@ -693,7 +727,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint32_t* mt, uint32_t* ctl, uin
         if (out.done) ((uint8_t*)out.done)[c.env] = (uint8_t)done;
     }
     e.store(st, c.env, c.lane);
-    if (c.lane == 0) ctl[c.env] = m.pos | (m.stale << 16);
+    if (c.lane == 0) m.save(ctl, c.env);
     if (rec.seq != nullptr && c.env == rec.env) {   // StepRecord (cs_engine.h): state words, fence, sequence number
         e.store(rec.words, 0, c.lane);
         __threadfence_system();
@@ -719,6 +753,7 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n
     }
 }
 
+template <bool PHX>
 __global__ __launch_bounds__(BLOCK, CS_DDZ_MINW) void k_rollout(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n, int T,
                                                     uint64_t seed, uint64_t t0, uint64_t env_base, cs_traj_out out,
                                                     Tab tb)
@@ -732,7 +767,7 @@ __global__ __launch_bounds__(BLOCK, CS_DDZ_MINW) void k_rollout(uint32_t* mt, ui
     const int lane = c.lane;
     Env e;
     e.load(st, c.env, lane, tb);
-    WaveMt m = wave_mt(mt, ctl, c.env);
+    auto m = wave_mt<PHX>(mt, ctl, c.env);
     if (e.over()) deal(e, m, lane);
     const uint64_t genv = env_base + (uint64_t)c.env;
     uint32_t rr_lane = 0;
@@ -778,7 +813,7 @@ __global__ __launch_bounds__(BLOCK, CS_DDZ_MINW) void k_rollout(uint32_t* mt, ui
         }
     }
     e.store(st, c.env, lane);
-    if (lane == 0) ctl[c.env] = m.pos | (m.stale << 16);
+    if (lane == 0) m.save(ctl, c.env);
 }
 
 // Test hook (cs_debug_ddz_legal): the legal set of player 0 holding `counts` -- leading when prev < 0, else following
@@ -843,14 +878,22 @@ hipError_t launch_debug_legal(const Buffers& b, const uint8_t* counts, const int
 
 hipError_t launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_reset, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, o, *(const Tab*)b.table,
-                       b.rec);
+    if (b.rng_mode == CS_RNG_PHILOX)
+        hipLaunchKernelGGL(k_reset<true>, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, o, *(const Tab*)b.table,
+                           b.rec);
+    else
+        hipLaunchKernelGGL(k_reset<false>, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, o, *(const Tab*)b.table,
+                           b.rec);
     return hipGetLastError();
 }
 hipError_t launch_step(const Buffers& b, const int32_t* a, const cs_step_out& o, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_step, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, a, o,
-                       *(const Tab*)b.table, b.rec);
+    if (b.rng_mode == CS_RNG_PHILOX)
+        hipLaunchKernelGGL(k_step<true>, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, a, o,
+                           *(const Tab*)b.table, b.rec);
+    else
+        hipLaunchKernelGGL(k_step<false>, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, a, o,
+                           *(const Tab*)b.table, b.rec);
     return hipGetLastError();
 }
 hipError_t launch_observe(const Buffers& b, int32_t p, const cs_step_out& o, hipStream_t s)
@@ -861,8 +904,12 @@ hipError_t launch_observe(const Buffers& b, int32_t p, const cs_step_out& o, hip
 hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
                           const cs_traj_out& o, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_rollout, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0, env_base, o,
-                       *(const Tab*)b.table);
+    if (b.rng_mode == CS_RNG_PHILOX)
+        hipLaunchKernelGGL(k_rollout<true>, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0, env_base, o,
+                           *(const Tab*)b.table);
+    else
+        hipLaunchKernelGGL(k_rollout<false>, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0, env_base, o,
+                           *(const Tab*)b.table);
     return hipGetLastError();
 }
 

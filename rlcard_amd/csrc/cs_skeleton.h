@@ -379,25 +379,35 @@ __global__ __launch_bounds__(BLOCK) void k_seed(uint32_t* mt, uint32_t* ctl, uin
     }
     MtLane m;
     m.init(mt, 0, 0);
+    // Philox mode (doudizhu's word layout, cs_doudizhu.hip WaveMt): the key in words 0..1, draw count 0 in word 2
+    const bool phx = prm.rng_mode == CS_RNG_PHILOX;   // uniform
     if (valid) {
         uint32_t* base = mt + env * MT_WORDS;
         const int kl = klen[i] == 2 ? 2 : 1;                    // validated on the host; never trust it here
-        mt_init_by_array(base + MT_N, keys + 2 * i, kl);        // S0 in block 1 (scratch)
-        mt_twist_serial(base + MT_N, base);                     // block 0 = twist(S0): numpy's first draws
-        m.base = base;
-        m.stale = 1;                                            // block 1 = twist(block 0), refilled below
+        if (phx) {
+            base[0] = keys[2 * i];
+            base[1] = kl == 2 ? keys[2 * i + 1] : 0u;
+            base[2] = 0u;
+        } else {
+            mt_init_by_array(base + MT_N, keys + 2 * i, kl);    // S0 in block 1 (scratch)
+            mt_twist_serial(base + MT_N, base);                 // block 0 = twist(S0): numpy's first draws
+            m.base = base;
+            m.stale = 1;                                        // block 1 = twist(block 0), refilled below
+        }
         G g;
         g.bind(scratch_of<G>(scr[threadIdx.x / WAVE], lane), prm);
         g.blank();
         g.store(st, n, env);
     }
-    if (flags & 1) {
-        if (valid) mt_twist_serial(m.base, m.base + MT_N);
-        m.stale = 0;
-    } else {
-        mt_refill_wave(m, lane);
+    if (!phx) {
+        if (flags & 1) {
+            if (valid) mt_twist_serial(m.base, m.base + MT_N);
+            m.stale = 0;
+        } else {
+            mt_refill_wave(m, lane);
+        }
     }
-    if (valid) ctl[env] = 0u;
+    if (valid) ctl[env] = phx ? CTL_PHILOX : 0u;
 }
 
 template <class G>
