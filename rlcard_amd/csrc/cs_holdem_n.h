@@ -123,12 +123,48 @@ __device__ __forceinline__ void holdem_judge(const uint32_t (&value)[P], const i
     }
 }
 
+#ifndef CS_DEALK_SWAR
+#define CS_DEALK_SWAR 1   // 0: the JV table below (A/B)
+#endif
 // The deal of a P-player hold'em game (limitholdem/dealer.py: shuffle 52, deal_card = pop): the K = 2P + 5 dealt
 // positions 51 .. 51 - K + 1 are fixed by the first K Fisher-Yates swaps, tracked in registers as in holdem_deal2
 // (JV[k] = j | card moved to j << 8); the other 51 - K draws only consume the stream. d[k] = card dealt k-th.
 template <int K, class Rng>
 __device__ __forceinline__ void holdem_deal_k(Rng& rng, uint32_t (&d)[K])
 {
+#if CS_DEALK_SWAR
+    // the K draws first (stream order), then every dealt position 51 - k traced back through the swaps q = K-1 .. 0
+    // four per word (SWAR byte compares, as holdem_deal2): ~K^2/4 word steps instead of the K^2/2 pairwise lookups
+    constexpr int NW = (K + 3) / 4;
+    uint32_t js[NW], X[NW];
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        js[w] = 0;
+        uint32_t x = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) x |= (4 * w + b < K ? 51u - (uint32_t)(4 * w + b) : 63u) << (8 * b);
+        X[w] = x;
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) js[k >> 2] |= rng.interval(51u - (uint32_t)k) << (8 * (k & 3));
+#pragma unroll
+    for (int q = K - 1; q >= 0; q--) {
+        const uint32_t I = (uint32_t)(51 - q) * 0x01010101u;
+        const uint32_t J = __builtin_amdgcn_perm(0u, js[q >> 2], (uint32_t)(q & 3) * 0x01010101u);
+        const uint32_t D = I ^ J;
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+            if (q > 4 * w + 3) continue;   // swap q never touches positions 51 - k, k < q
+            const uint32_t both = ((X[w] ^ I) + 0x7F7F7F7Fu) & ((X[w] ^ J) + 0x7F7F7F7Fu);
+            const uint32_t m = ~both & 0x80808080u;
+            X[w] ^= D & (m - (m >> 7));
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) d[k] = (X[k >> 2] >> (8 * (k & 3))) & 63u;
+    rng.skip_intervals(51u - K);
+    return;
+#endif
     uint32_t JV[K];
 #pragma unroll
     for (int k = 0; k < K; k++) {

@@ -1,6 +1,6 @@
 """A/B timing of k_rollout kernel variants (cs_debug_set_kernel_flags) interleaved in ONE process (rule 24).
   python tools/ab_rollout.py GAME N T flagsA flagsB ...
-AB_WARM (env, default 40) launches run first so the MT streams reach their steady block-refill rate (every env starts
+AB_PLAYERS (env): game_num_players. AB_WARM (env, default 40) launches run first so the MT streams reach their steady block-refill rate (every env starts
 at stream position 0 after seeding, so the first refills all come ~624 draws in)."""
 import os
 import sys
@@ -13,7 +13,8 @@ from rlcard_amd import VecEnv  # noqa: E402
 
 game, n, T = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 variants = [int(x) for x in sys.argv[4:]] or [0, 2, 4, 6]
-v = VecEnv(game, n, seed=42, device=0)
+np_ = int(os.environ.get('AB_PLAYERS', '0'))   # game_num_players (0: the game's default)
+v = VecEnv(game, n, seed=42, device=0, config={'game_num_players': np_} if np_ else None)
 v.reset()
 tr = v.new_traj_out(T)
 t = 0
