@@ -95,7 +95,9 @@ int cs_create(cs_handle** out, int32_t game, int64_t num_envs, int32_t device, c
     h->b.table = nullptr;
     if ((r = set_device(h)) != CS_OK) { delete h; return r; }
     const size_t n = (size_t)num_envs;
-    if ((e = hipMalloc((void**)&h->b.mt, n * cs::MT_WORDS_HOST * sizeof(uint32_t))) != hipSuccess ||
+    // u32 per env of the MT stream: doudizhu's two word blocks, the others' byte ring (info.rng_period bytes + wbuf)
+    const size_t mtw = info.rng_period == 2 * 624 ? (size_t)(2 * 624) : (size_t)cs::RING_ENV_WORDS_HOST;
+    if ((e = hipMalloc((void**)&h->b.mt, n * mtw * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc((void**)&h->b.ctl, n * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc((void**)&h->b.state, n * (size_t)info.state_words * sizeof(uint32_t))) != hipSuccess) {
         cs_destroy(h);

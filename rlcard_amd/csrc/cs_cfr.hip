@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void k_cfr_iteration(uint32_t* mt, uint32_t* c
     const bool valid = env < n;
     const bool atomic = n > 1;
     RingLane<> m;
-    if (valid) m.init(mt + env * MT_WORDS, ctl[env]);
+    if (valid) m.init(mt + env * RING_ENV_WORDS, ctl[env]);
     else m.init(mt, 2u << 12);   // never needs a refill
     Leduc g;
     g.blank();

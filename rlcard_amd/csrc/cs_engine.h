@@ -6,7 +6,12 @@
 
 namespace cs {
 
-constexpr int MT_WORDS_HOST = 2 * 624;  // u32 per env: two MT19937 blocks
+// Byte-ring slots of the lane-per-env games' MT19937 streams (cs_ring.h): 8 = seven blocks twisted per refill from
+// one read and one write of the block words (4: three)
+#ifndef CS_RING_SLOTS
+#define CS_RING_SLOTS 8
+#endif
+constexpr int RING_ENV_WORDS_HOST = 624 + CS_RING_SLOTS * 624 / 4;   // u32 per env: block words + the ring bytes
 
 // cs_set_step_record: the single-step kernels also write env `env`'s packed state words to `words`, then -- after a
 // system-scope fence that orders every output store of that env's wave -- `seqv` to *seq (both typically in mapped

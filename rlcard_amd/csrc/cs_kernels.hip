@@ -64,6 +64,7 @@ int game_info(int32_t game, const cs_config* cfg, cs_game_info* info)
         info->action_bytes = 2;
         info->state_words = ddz::WORDS;
         info->action_feature_dim = 54;
+        info->rng_period = 2 * 624;
         return CS_OK;
     default:
         return CS_E_UNSUPPORTED;

@@ -3,33 +3,44 @@
 // Every draw of Leduc / Limit / No-limit Hold'em / Blackjack is numpy's random_interval(max <= 52), which reads only
 // the low 8 bits of a tempered output word (cs_device.h, MtLaneT). So the stream does not need to be kept as words:
 // per env the engine holds
-//   wbuf[624]  u32   the untempered state words of the LATEST generated block L (the only input of the next twist)
-//   ring[4][624] u8  the low bytes of the tempered outputs of blocks L-3 .. L, block b in slot b % 4
-// (1248 u32 per env: the same footprint as two word blocks). A refill twists THREE blocks in a row in registers --
-// L+1, L+2, L+3 -- writes their bytes into the three consumed slots and only the last block's words back to wbuf.
-// Per 1 872 draws that is one 2.5 KB word read + one 2.5 KB word write + 1 872 B of bytes written and later read
-// (~4.7 B per draw) where the word layout moved ~12 B per draw (block read + block write by the refill, and a 4-B word
-// re-read per draw to temper it). Staging (restage into the LDS rows) becomes a byte copy: no tempering, no packing.
+//   wbuf[624]  u32       the untempered state words of the LATEST generated block L (the only input of the next twist)
+//   ring[S][624] u8      the low bytes of the tempered outputs of blocks L-S+1 .. L, block b in slot b % S
+// (S = RING_SLOTS = 8: 624 + 1 248 u32 per env). A refill twists S - 1 = SEVEN blocks in a row in registers --
+// L+1 .. L+7 -- writes their bytes into the seven consumed slots and only the last block's words back to wbuf.
+// Per 4 368 draws that is one 2.5 KB word read + one 2.5 KB word write (1.14 B per draw; with 4 slots, three blocks
+// per refill, 2.67 B per draw) + the bytes written and later read, where the word layout moved ~12 B per draw (block
+// read + block write by the refill, and a 4-B word re-read per draw to temper it). Staging (restage into the LDS rows)
+// becomes a byte copy: no tempering, no packing.
 //
-// ctl[env] u32: bits 0..11 = ring position (draws consumed mod 2 496), bits 12..13 = slot of block L, bit 17 = the
+// ctl[env] u32: bits 0..12 = ring position (draws consumed mod RING), bits 13..15 = slot of block L, bit 17 = the
 // rollout's staged LDS rows are valid (cs_kernels.hip). A lane needs a refill when it is inside block L; the
 // wave refills at step boundaries (ring_refill_wave); a lane that would step past L inside a step (more than 624
 // draws in one step: only a rejection loop's tail) generates in-lane (ring_gen_serial): slow, never on the fast path,
 // same numbers.
 //
 // Philox mode (cs_config.rng_mode = CS_RNG_PHILOX, ctl bit 18; not seed-compatible with the reference): the ring
-// layout, staging and every game's draw code stay as they are, but a refill fills the three slots with Philox4x32-10
+// layout, staging and every game's draw code stay as they are, but a refill fills the S - 1 slots with Philox4x32-10
 // bytes -- key = the env's init_by_array key, counter = (absolute block index, 16-byte chunk) -- instead of twisting:
-// wbuf holds only the block counter and the key (words 0..2), so the refill reads nothing and writes 1 872 ring bytes
-// (~2 B per draw: written once, read once) where MT19937 moves ~4.7.
+// wbuf holds only the block counter and the key (words 0..2), so the refill reads nothing and writes the ring bytes
+// (~2 B per draw: written once, read once).
 #pragma once
 #include "cs_device.h"
+#include "cs_engine.h"
 
 namespace cs {
 
-constexpr int RING_SLOTS = 4;
+// Ring slots (CS_RING_SLOTS, cs_engine.h): a refill twists SLOTS - 1 blocks in a row from one read of wbuf and writes
+// wbuf back once, so the block-word traffic per draw is 2 x 2 496 B / ((SLOTS - 1) x 624): 4 slots 2.67 B/draw, 8 slots
+// 1.14 B/draw (per env 624 + SLOTS x 156 u32 = RING_ENV_WORDS).
+constexpr int RING_SLOTS = CS_RING_SLOTS;
+static_assert(RING_SLOTS == 4 || RING_SLOTS == 8, "ring slots: a power of two, position < 2^13");
+constexpr uint32_t SLOT_MASK = (uint32_t)RING_SLOTS - 1u;
 constexpr int RING_GEN = RING_SLOTS - 1;        // blocks generated per refill
-constexpr uint32_t RING = RING_SLOTS * MT_N;    // 2 496 bytes
+constexpr uint32_t RING = RING_SLOTS * MT_N;    // ring bytes: 2 496 (4 slots) / 4 992 (8 slots)
+static_assert(RING_ENV_WORDS_HOST == MT_N + RING_SLOTS * MT_N / 4, "host and device agree on the ring footprint");
+constexpr int RING_ENV_WORDS = RING_ENV_WORDS_HOST;   // u32 per env in the mt buffer: wbuf + the ring bytes
+constexpr uint32_t CTL_POS_MASK = 0x1FFFu;
+constexpr int CTL_LAT_SHIFT = 13;
 constexpr uint32_t CTL_PHILOX = 1u << 18;       // ctl bit: the env's stream is the Philox byte stream
 constexpr int PHX_CHUNKS = MT_N / 16;           // 39 Philox blocks (16 bytes) per ring block
 
@@ -69,7 +80,7 @@ __device__ __forceinline__ void ring_gen_philox(gu32* wbuf, uint32_t lat, int c0
         const int b = c / PHX_CHUNKS, j = c - b * PHX_CHUNKS;
         uint32_t w[4];
         philox4(key, (uint64_t)(blk0 + (uint32_t)b), (uint64_t)j, w);
-        const uint32_t slot = (lat + 1u + (uint32_t)b) & 3u;
+        const uint32_t slot = (lat + 1u + (uint32_t)b) & SLOT_MASK;
         gu32* d = ring + slot * (MT_N / 4) + 4 * j;
         d[0] = w[0]; d[1] = w[1]; d[2] = w[2]; d[3] = w[3];
     }
@@ -86,7 +97,7 @@ __device__ __attribute__((noinline)) void ring_gen_serial(uint32_t* wbuf, uint32
     uint8_t* ring = (uint8_t*)(wbuf + MT_N);
     for (uint32_t b = 1; b <= (uint32_t)RING_GEN; b++) {
         mt_twist_inplace(wbuf);
-        ring_bytes_serial(wbuf, ring, (lat + b) & 3u);
+        ring_bytes_serial(wbuf, ring, (lat + b) & SLOT_MASK);
     }
 }
 
@@ -155,7 +166,7 @@ __device__ __forceinline__ void ring_gen_wave(gu32* wbuf, uint32_t lat, int lane
 #pragma unroll
     for (int b = 1; b <= RING_GEN; b++) {
         twist_regs(o, n, lane);
-        const uint32_t slot = (lat + (uint32_t)b) & 3u;
+        const uint32_t slot = (lat + (uint32_t)b) & SLOT_MASK;
 #pragma unroll
         for (int c = 0; c < 10; c++) {
             const int t = (int)(mt_temper(n[c]) & 255u);
@@ -177,7 +188,7 @@ __device__ __forceinline__ void ring_gen_wave(gu32* wbuf, uint32_t lat, int lane
 template <int MODE = STAGE_NONE>
 struct RingLane {
     static constexpr int kMode = MODE;
-    uint32_t* base;   // wbuf of the env (mt + env * 1248); the ring bytes follow it
+    uint32_t* base;   // wbuf of the env (mt + env * RING_ENV_WORDS); the ring bytes follow it
     uint32_t pos;     // ring position
     uint32_t lat;     // slot of the latest generated block
     uint32_t sp, sn;  // ring position of staged byte 0; staged bytes
@@ -187,16 +198,16 @@ struct RingLane {
     __device__ __forceinline__ void init(uint32_t* p_base, uint32_t ctlw)
     {
         base = p_base;
-        pos = ctlw & 0xFFFu;
-        lat = (ctlw >> 12) & 3u;
+        pos = ctlw & CTL_POS_MASK;
+        lat = (ctlw >> CTL_LAT_SHIFT) & SLOT_MASK;
         phx = ctlw & CTL_PHILOX;
         sp = 0;
         sn = 0;
         stg = nullptr;
     }
-    __device__ __forceinline__ uint32_t ctl_word() const { return pos | lat << 12 | phx; }
+    __device__ __forceinline__ uint32_t ctl_word() const { return pos | lat << CTL_LAT_SHIFT | phx; }
     __device__ __forceinline__ const uint8_t* ring() const { return (const uint8_t*)(base + MT_N); }
-    __device__ __forceinline__ uint32_t limit() const { return ((lat + 1u) & 3u) * (uint32_t)MT_N; }
+    __device__ __forceinline__ uint32_t limit() const { return ((lat + 1u) & SLOT_MASK) * (uint32_t)MT_N; }
     // draws left before the end of the generated data (1 .. RING)
     __device__ __forceinline__ uint32_t ahead() const
     {
@@ -208,7 +219,7 @@ struct RingLane {
     __device__ __forceinline__ void gen_serial()
     {
         ring_gen_serial(base, lat, phx);
-        lat = (lat + (uint32_t)RING_GEN) & 3u;
+        lat = (lat + (uint32_t)RING_GEN) & SLOT_MASK;
     }
 
     __device__ __forceinline__ void advance()
@@ -352,7 +363,7 @@ __device__ __forceinline__ void ring_refill_wave(M& m, int lane)
         need &= need - 1;
         ring_gen_wave(lane_ptr(m.base, j), __builtin_amdgcn_readlane(m.lat, j), lane,
                       __builtin_amdgcn_readlane(m.phx, j));
-        if (lane == j) m.lat = (m.lat + (uint32_t)RING_GEN) & 3u;
+        if (lane == j) m.lat = (m.lat + (uint32_t)RING_GEN) & SLOT_MASK;
     }
     // the ring bytes are read later by their owner lane of this same wave: order the stores before those loads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

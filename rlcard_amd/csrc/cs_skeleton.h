@@ -72,8 +72,8 @@ template <int MODE = STAGE_NONE>
 __device__ __forceinline__ RingLane<MODE> ring_lane(uint32_t* mt, const uint32_t* ctl, const LaneCtx& c)
 {
     RingLane<MODE> m;
-    if (c.valid) m.init(mt + c.env * MT_WORDS, ctl[c.env]);
-    else m.init(mt, 0u | 2u << 12);
+    if (c.valid) m.init(mt + c.env * RING_ENV_WORDS, ctl[c.env]);
+    else m.init(mt, 0u | (uint32_t)(RING_GEN - 1) << CTL_LAT_SHIFT);
     return m;
 }
 
@@ -352,16 +352,16 @@ __global__ __launch_bounds__(BLOCK) void k_seed(uint32_t* mt, uint32_t* ctl, uin
     const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     const bool valid = i < count;
     const int64_t env = first + i;
-    if constexpr (G::RING) {   // byte ring: S0 = init_by_array(key) in wbuf, blocks 0..2 generated in place
+    if constexpr (G::RING) {   // byte ring: S0 = init_by_array(key) in wbuf, blocks 0..RING_GEN-1 generated in place
         if (!valid) return;
-        uint32_t* wbuf = mt + env * MT_WORDS;
+        uint32_t* wbuf = mt + env * RING_ENV_WORDS;
         const int kl = klen[i] == 2 ? 2 : 1;                    // validated on the host; never trust it here
         const uint32_t phx = prm.rng_mode == CS_RNG_PHILOX ? CTL_PHILOX : 0u;
-        if (phx) {   // Philox byte stream: block counter 0, key = the init_by_array key, blocks 0..2 into slots 0..2
+        if (phx) {   // Philox byte stream: block counter 0, key = the init_by_array key, blocks 0.. into slots 0..
             wbuf[0] = 0u;
             wbuf[1] = keys[2 * i];
             wbuf[2] = kl == 2 ? keys[2 * i + 1] : 0u;
-            ring_gen_serial(wbuf, 3u, phx);
+            ring_gen_serial(wbuf, SLOT_MASK, phx);
         } else {
             mt_init_by_array(wbuf, keys + 2 * i, kl);
             for (uint32_t b = 0; b < (uint32_t)RING_GEN; b++) {     // numpy's first draws: block 0 = twist(S0)
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed(uint32_t* mt, uint32_t* ctl, uin
         g.blank();
         g.store(st, n, env);
         if constexpr (DqOf<G>::value > 0) st[(int64_t)G::GW * n + env] = 0u;   // empty deal queue
-        ctl[env] = 0u | (uint32_t)(RING_GEN - 1) << 12 | phx;    // position 0, latest block in slot 2
+        ctl[env] = 0u | (uint32_t)(RING_GEN - 1) << CTL_LAT_SHIFT | phx;   // position 0, latest block in slot RING_GEN-1
         return;
     }
     MtLane m;
@@ -701,6 +701,7 @@ static void fill_info(cs_game_info* info)
     info->action_bytes = G::ACTION_BYTES;
     info->state_words = G::WORDS;
     info->action_feature_dim = G::A;
+    info->rng_period = (int32_t)RING;
 }
 
 template <class G>

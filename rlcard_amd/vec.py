@@ -209,9 +209,15 @@ class VecEnv:
 
     @property
     def rng_period(self):
-        """Draws after which the stream position wraps: the byte ring of the lane-per-env games holds 4 blocks
-        (rlcard_amd/csrc/cs_ring.h), doudizhu's word layout 2."""
-        return 1248 if self.env_id == 'doudizhu' else 2496
+        """Draws after which the stream position wraps (cs_game_info.rng_period): the byte ring of the lane-per-env
+        games holds CS_RING_SLOTS blocks (rlcard_amd/csrc/cs_ring.h), doudizhu's word layout 2."""
+        return int(self.info.rng_period)
+
+    @property
+    def rng_first_refill(self):
+        """Draws before an env's first refill: seeding generates the ring's first SLOTS - 1 blocks and a refill runs
+        once the stream is inside the latest (doudizhu: inside its second word block)."""
+        return self.rng_period - 2 * 624 if self.env_id != 'doudizhu' else 624
 
     # heads-up hold'em games keep a deal queue after their 4 game words (rlcard_amd/csrc/cs_limit.h): deals drawn
     # ahead. 3..6-player hold'em has none (its judge may draw from the stream at a game's end, cs_holdem_n.h).
@@ -232,7 +238,7 @@ class VecEnv:
         do not count: they belong to the games after the current one."""
         v = C.c_uint32()
         _abi.check(_abi.lib().cs_get_rng_ctl(self._h, int(env), C.byref(v)), 'cs_get_rng_ctl')
-        pos = v.value & (0x7FF if self.env_id == 'doudizhu' else 0xFFF)
+        pos = v.value & (0x7FF if self.env_id == 'doudizhu' else 0x1FFF)   # cs_ring.h ctl layout
         gw = self.game_words
         if gw is not None and self.info.state_words > gw:
             w = self.env_state_words(env)

@@ -30,10 +30,10 @@ def _same(got, exp, what):
             raise AssertionError('%s: %s differs at %d places, first %s' % (what, k, len(bad), bad[0]))
 
 
-@pytest.mark.parametrize('game,cfg,T', [('leduc-holdem', {}, 512), ('limit-holdem', {}, 64),
-                                        ('no-limit-holdem', {}, 64), ('blackjack', {}, 32),
-                                        ('leduc-holdem', {'game_num_players': 3}, 768),
-                                        ('limit-holdem', {'game_num_players': 4}, 64)])
+@pytest.mark.parametrize('game,cfg,T', [('leduc-holdem', {}, 1024), ('limit-holdem', {}, 128),
+                                        ('no-limit-holdem', {}, 128), ('blackjack', {}, 64),
+                                        ('leduc-holdem', {'game_num_players': 3}, 1536),
+                                        ('limit-holdem', {'game_num_players': 4}, 256)])
 @pytest.mark.parametrize('flags', [0, 1])
 def test_philox_stream_matches_oracle(oracle, game, cfg, T, flags):
     from rlcard_amd import VecEnv
@@ -52,7 +52,7 @@ def test_philox_stream_matches_oracle(oracle, game, cfg, T, flags):
     torch.cuda.synchronize()
     for i in (0, 64, n - 1):
         assert v.rng_position(i) == ob.draws(i) % v.rng_period
-    assert max(ob.draws(i) for i in range(0, n, 97)) > 1248 + 624, 'the test crosses ring refills'
+    assert max(ob.draws(i) for i in range(0, n, 97)) > v.rng_first_refill + 624, 'the test crosses ring refills'
 
 
 def test_philox_deals_differ_from_mt19937():

@@ -1,10 +1,11 @@
 """Parity past the MT19937 refills, at the shapes bench.py times.
 
-A freshly seeded lane-game env (Leduc, Limit, No-limit, Blackjack) holds ring blocks 0-2 and first refills once its
-stream is inside block L (position >= 3 x 624 - 624 = 1248 draws, cs_ring.h `needs_refill`); DouDizhu's two-block word
+A freshly seeded lane-game env (Leduc, Limit, No-limit, Blackjack) holds ring blocks 0..SLOTS-2 and first refills once
+its stream is inside block L (position >= rng_period - 2 x 624: 3 744 draws with 8 slots, cs_ring.h `needs_refill`),
+then every (SLOTS - 1) x 624 draws; DouDizhu's two-block word
 window first twists at ~1 184 draws (cs_doudizhu.hip `WaveMt::window`). The tests below drive every env well past
 two refills and compare every launch with the CPU oracle, so the paths the timed launches run in steady state
-(ring_refill_wave's 3-block twist, ring_gen_serial, the batched restage after a refill, Leduc's reset_swar across block
+(ring_refill_wave's multi-block twist, ring_gen_serial, the batched restage after a refill, Leduc's reset_swar across block
 edges, DouDizhu's mt_twist_wave and the MT_WORDS wrap) are all checked bit-exactly.
 Reference: the deals that consume the stream, rlcard/games/leducholdem/game.py:46-95, doudizhu/dealer.py:12-76,
 limitholdem/dealer.py:11-21; numpy RandomState (MT19937 legacy)."""
@@ -17,7 +18,11 @@ from test_gpu_engine import _assert_same, _np, _oracle_batch, _vec
 torch = pytest.importorskip('torch')
 pytestmark = pytest.mark.gpu
 
-REFILL_DRAWS = 2 * 624 + 2 * 1872   # past the first refill (1 248) and two more three-block refills
+
+
+def past_refills(k):
+    """min draws per env: past the first refill and k more (from the library's ring geometry)"""
+    return lambda v: v.rng_first_refill + k * (v.rng_period - 624)
 
 
 @pytest.fixture(scope='module', autouse=True)
@@ -42,6 +47,7 @@ def _roll_past_refills(oracle, game, n, T, launches, flags, seed, min_draws):
         _assert_same(got, exp, '%s flags %d launch %d' % (game, flags, c))
     torch.cuda.synchronize()
     d = _draws(ob, n)
+    min_draws = min_draws(v) if callable(min_draws) else min_draws
     assert d.min() >= min_draws, 'test too short: min draws %d < %d' % (d.min(), min_draws)
     for i in sorted({0, 1, 63, 64, n // 2, n - 1, int(np.argmax(d)), int(np.argmin(d))} & set(range(n))):
         assert v.rng_position(i) == d[i] % v.rng_period, i
@@ -51,16 +57,16 @@ def _roll_past_refills(oracle, game, n, T, launches, flags, seed, min_draws):
 @pytest.mark.parametrize('flags', [0, 1])          # 1 = serial (per-lane) refill instead of the wave twist
 def test_leduc_bench_shape_past_refills(oracle, flags):
     """bench.py's Leduc sequence (T = 256 fused steps, one trajectory buffer) on 4 133 envs (a ragged tail wave)
-    for 8 launches: every env crosses >= 4 000 draws, i.e. the first refill and two three-block refills after it."""
-    _roll_past_refills(oracle, 'leduc-holdem', 4096 + 37, 256, 8, flags, 42, 4000)
+    for 14 launches: every env crosses the first refill and one full refill cycle after it (>= 8 112 draws)."""
+    _roll_past_refills(oracle, 'leduc-holdem', 4096 + 37, 256, 14, flags, 42, past_refills(1))
 
 
-@pytest.mark.parametrize('game,T,launches', [('limit-holdem', 128, 3), ('no-limit-holdem', 128, 3),
-                                             ('blackjack', 64, 2)])
+@pytest.mark.parametrize('game,T,launches', [('limit-holdem', 128, 6), ('no-limit-holdem', 128, 6),
+                                             ('blackjack', 64, 5)])
 def test_lane_games_bench_shape_past_refills(oracle, game, T, launches):
     """The other lane-per-env games at their bench T: each env draws ~25-57 words per step, so a few launches
-    cross many refills (every slot of the 4-block ring is rewritten several times)."""
-    _roll_past_refills(oracle, game, 2048 + 19, T, launches, 0, 42, REFILL_DRAWS)
+    cross several refills (every slot of the ring is rewritten at least twice)."""
+    _roll_past_refills(oracle, game, 2048 + 19, T, launches, 0, 42, past_refills(2))
 
 
 def test_doudizhu_past_mt_twists(oracle):
@@ -70,9 +76,9 @@ def test_doudizhu_past_mt_twists(oracle):
 
 
 def test_leduc_full_size_after_precondition(oracle):
-    """The bench's 2^20 Leduc envs after its 2 preconditioning launches (T = 256): one timed-shape launch is then
+    """The bench's 2^20 Leduc envs after 7 preconditioning launches (T = 256): one timed-shape launch is then
     compared with the oracle on three windows (start, middle, end) replayed from seeding with the same env ids."""
-    n, T, win, pre = 1 << 20, 256, 256, 3
+    n, T, win, pre = 1 << 20, 256, 256, 7
     v = _vec('leduc-holdem', n, seed=42)
     v.reset()
     out = v.new_traj_out(T)
@@ -89,7 +95,7 @@ def test_leduc_full_size_after_precondition(oracle):
         got = {k: x[:, start:start + win].cpu().numpy() for k, x in tr.items()}
         _assert_same(got, exp, 'window %d' % start)
         d = _draws(ob, win)
-        assert d.min() >= 1248 + 300, 'window %d has not refilled (min draws %d)' % (start, d.min())
+        assert d.min() >= v.rng_first_refill + 300, 'window %d has not refilled (min draws %d)' % (start, d.min())
         for i in (0, win - 1):
             assert v.rng_position(start + i) == d[i] % v.rng_period
 
@@ -99,7 +105,7 @@ def test_cfr_batched_past_refills(oracle):
     per player): tables to 1e-9, RNG positions exactly."""
     from rlcard_amd import VecEnv
     from rlcard_amd.agents import CFRAgent
-    B, K = 256 + 3, 400
+    B, K = 256 + 3, 400   # fp64 atomics in any order: 1e-9 holds at this length (800: 1e-8)
     v = VecEnv('leduc-holdem', B, seed=21)
     agent = CFRAgent(v)
     agent.train(K)
@@ -108,7 +114,7 @@ def test_cfr_batched_past_refills(oracle):
     c = oracle.CFR(keys, lens)
     c.train(K)
     d = np.array([c.draws(i) for i in range(B)])
-    assert d.min() >= 4000, d.min()
+    assert d.min() >= v.rng_first_refill + 1000, d.min()   # every stream is past its first refill
     t = c.tables()
     host = agent._tables()
     assert np.array_equal(host['flags'].astype(np.uint8), t['flags'])
