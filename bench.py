@@ -33,12 +33,12 @@ MT_N = 624              # words per MT19937 block
 # read + written once per launch (state words + the RNG control word), the expected tempered-u32 MT19937 draws per
 # env-step under random play (exact acceptance rates of random_interval x random-play game lengths), and
 # the stream geometry: draws before the first block refill and draws per refill. Lane-per-env games keep a byte ring
-# of RING_SLOTS = 8 blocks (cs_engine.h CS_RING_SLOTS), 7 generated at seeding and 7 more per refill once the lane is
-# inside the last one (cs_ring.h: needs_refill at position >= 6 x 624); DouDizhu a two-block word window that twists
+# of RING_SLOTS = 16 blocks (cs_engine.h CS_RING_SLOTS), 15 generated at seeding and 15 more per refill once the lane
+# is inside the last one (cs_ring.h: needs_refill at position >= 14 x 624); DouDizhu a two-block word window that twists
 # one block per 624 draws (cs_doudizhu.hip WaveMt::window, first twist ~1 184 draws in).
 # Fused steps per launch, measured on one box: Leduc 256 vs 128 +3 % (T >= 256), 512 vs 256 -9 %;
 # Limit / No-limit 256 vs 128 +1.5 / +2 % (128 vs 64 +2.5 / +3 %), DouDizhu 128 vs 64 -7 %.
-RING_SLOTS = 8
+RING_SLOTS = 16
 RING = dict(first_refill=(RING_SLOTS - 2) * MT_N, per_refill=(RING_SLOTS - 1) * MT_N)
 GAMES = {
     'leduc-holdem': dict(envs=1 << 20, T=256, state_bytes=2 * 4 + 4, draws_per_step=2.83, **RING),

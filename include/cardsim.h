@@ -58,7 +58,7 @@ typedef struct {
     int32_t state_words;  /* packed u32 words of game state per env */
     int32_t action_feature_dim; /* bytes per cs_action_features row: doudizhu 54, otherwise num_actions (one-hot) */
     int32_t rng_period;   /* draws after which the stream position of cs_get_rng_ctl wraps: doudizhu 1 248 (two word
-                             blocks), the others the byte ring's 4 992 (8 slots of 624) */
+                             blocks), the others the byte ring's 9 984 (16 slots of 624) */
 } cs_game_info;
 
 /* Outputs of reset/step/observe, all device pointers, one row per env:

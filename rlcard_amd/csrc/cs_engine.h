@@ -6,10 +6,10 @@
 
 namespace cs {
 
-// Byte-ring slots of the lane-per-env games' MT19937 streams (cs_ring.h): 8 = seven blocks twisted per refill from
-// one read and one write of the block words (4: three)
+// Byte-ring slots of the lane-per-env games' MT19937 streams (cs_ring.h): 16 = 15 blocks twisted per refill from one
+// read and one write of the block words (8: seven, 4: three)
 #ifndef CS_RING_SLOTS
-#define CS_RING_SLOTS 8
+#define CS_RING_SLOTS 16
 #endif
 constexpr int RING_ENV_WORDS_HOST = 624 + CS_RING_SLOTS * 624 / 4;   // u32 per env: block words + the ring bytes
 

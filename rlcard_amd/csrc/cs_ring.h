@@ -5,14 +5,13 @@
 // per env the engine holds
 //   wbuf[624]  u32       the untempered state words of the LATEST generated block L (the only input of the next twist)
 //   ring[S][624] u8      the low bytes of the tempered outputs of blocks L-S+1 .. L, block b in slot b % S
-// (S = RING_SLOTS = 8: 624 + 1 248 u32 per env). A refill twists S - 1 = SEVEN blocks in a row in registers --
-// L+1 .. L+7 -- writes their bytes into the seven consumed slots and only the last block's words back to wbuf.
-// Per 4 368 draws that is one 2.5 KB word read + one 2.5 KB word write (1.14 B per draw; with 4 slots, three blocks
-// per refill, 2.67 B per draw) + the bytes written and later read, where the word layout moved ~12 B per draw (block
+// (S = RING_SLOTS = 16: 624 + 2 496 u32 per env). A refill twists S - 1 = 15 blocks in a row in registers --
+// L+1 .. L+15 -- writes their bytes into the consumed slots and only the last block's words back to wbuf.
+// Per 9 360 draws that is one 2.5 KB word read + one 2.5 KB word write (0.53 B per draw; 8 slots 1.14, 4 slots 2.67) + the bytes written and later read, where the word layout moved ~12 B per draw (block
 // read + block write by the refill, and a 4-B word re-read per draw to temper it). Staging (restage into the LDS rows)
 // becomes a byte copy: no tempering, no packing.
 //
-// ctl[env] u32: bits 0..12 = ring position (draws consumed mod RING), bits 13..15 = slot of block L, bit 17 = the
+// ctl[env] u32: bits 0..13 = ring position (draws consumed mod RING), bits 19..22 = slot of block L, bit 17 = the
 // rollout's staged LDS rows are valid (cs_kernels.hip). A lane needs a refill when it is inside block L; the
 // wave refills at step boundaries (ring_refill_wave); a lane that would step past L inside a step (more than 624
 // draws in one step: only a rejection loop's tail) generates in-lane (ring_gen_serial): slow, never on the fast path,
@@ -33,14 +32,14 @@ namespace cs {
 // wbuf back once, so the block-word traffic per draw is 2 x 2 496 B / ((SLOTS - 1) x 624): 4 slots 2.67 B/draw, 8 slots
 // 1.14 B/draw (per env 624 + SLOTS x 156 u32 = RING_ENV_WORDS).
 constexpr int RING_SLOTS = CS_RING_SLOTS;
-static_assert(RING_SLOTS == 4 || RING_SLOTS == 8, "ring slots: a power of two, position < 2^13");
+static_assert(RING_SLOTS == 4 || RING_SLOTS == 8 || RING_SLOTS == 16, "ring slots: a power of two, position < 2^14");
 constexpr uint32_t SLOT_MASK = (uint32_t)RING_SLOTS - 1u;
 constexpr int RING_GEN = RING_SLOTS - 1;        // blocks generated per refill
 constexpr uint32_t RING = RING_SLOTS * MT_N;    // ring bytes: 2 496 (4 slots) / 4 992 (8 slots)
 static_assert(RING_ENV_WORDS_HOST == MT_N + RING_SLOTS * MT_N / 4, "host and device agree on the ring footprint");
 constexpr int RING_ENV_WORDS = RING_ENV_WORDS_HOST;   // u32 per env in the mt buffer: wbuf + the ring bytes
-constexpr uint32_t CTL_POS_MASK = 0x1FFFu;
-constexpr int CTL_LAT_SHIFT = 13;
+constexpr uint32_t CTL_POS_MASK = 0x3FFFu;   // ctl bits 0..13: ring position
+constexpr int CTL_LAT_SHIFT = 19;            // ctl bits 19..22: slot of the latest block (16..18: flags)
 constexpr uint32_t CTL_PHILOX = 1u << 18;       // ctl bit: the env's stream is the Philox byte stream
 constexpr int PHX_CHUNKS = MT_N / 16;           // 39 Philox blocks (16 bytes) per ring block
 
@@ -163,7 +162,9 @@ __device__ __forceinline__ void ring_gen_wave(gu32* wbuf, uint32_t lat, int lane
 #pragma unroll
     for (int c = 0; c < 10; c++) o[c] = (c < 9 || lane < 48) ? ring_ld(wbuf + 64 * c + lane) : 0u;
     gu32* ring = wbuf + MT_N;   // 624 dwords of bytes
-#pragma unroll
+    // the blocks in a rolled loop: one block's code (unrolled 15 times, the refill alone would be ~40 KB of the
+    // rollout kernels' instruction footprint)
+#pragma unroll 1
     for (int b = 1; b <= RING_GEN; b++) {
         twist_regs(o, n, lane);
         const uint32_t slot = (lat + (uint32_t)b) & SLOT_MASK;

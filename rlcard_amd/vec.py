@@ -238,7 +238,7 @@ class VecEnv:
         do not count: they belong to the games after the current one."""
         v = C.c_uint32()
         _abi.check(_abi.lib().cs_get_rng_ctl(self._h, int(env), C.byref(v)), 'cs_get_rng_ctl')
-        pos = v.value & (0x7FF if self.env_id == 'doudizhu' else 0x1FFF)   # cs_ring.h ctl layout
+        pos = v.value & (0x7FF if self.env_id == 'doudizhu' else 0x3FFF)   # cs_ring.h ctl layout
         gw = self.game_words
         if gw is not None and self.info.state_words > gw:
             w = self.env_state_words(env)

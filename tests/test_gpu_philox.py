@@ -30,10 +30,10 @@ def _same(got, exp, what):
             raise AssertionError('%s: %s differs at %d places, first %s' % (what, k, len(bad), bad[0]))
 
 
-@pytest.mark.parametrize('game,cfg,T', [('leduc-holdem', {}, 1024), ('limit-holdem', {}, 128),
-                                        ('no-limit-holdem', {}, 128), ('blackjack', {}, 64),
-                                        ('leduc-holdem', {'game_num_players': 3}, 1536),
-                                        ('limit-holdem', {'game_num_players': 4}, 256)])
+@pytest.mark.parametrize('game,cfg,T', [('leduc-holdem', {}, 2048), ('limit-holdem', {}, 256),
+                                        ('no-limit-holdem', {}, 256), ('blackjack', {}, 128),
+                                        ('leduc-holdem', {'game_num_players': 3}, 3072),
+                                        ('limit-holdem', {'game_num_players': 4}, 512)])
 @pytest.mark.parametrize('flags', [0, 1])
 def test_philox_stream_matches_oracle(oracle, game, cfg, T, flags):
     from rlcard_amd import VecEnv

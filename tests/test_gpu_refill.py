@@ -57,12 +57,12 @@ def _roll_past_refills(oracle, game, n, T, launches, flags, seed, min_draws):
 @pytest.mark.parametrize('flags', [0, 1])          # 1 = serial (per-lane) refill instead of the wave twist
 def test_leduc_bench_shape_past_refills(oracle, flags):
     """bench.py's Leduc sequence (T = 256 fused steps, one trajectory buffer) on 4 133 envs (a ragged tail wave)
-    for 14 launches: every env crosses the first refill and one full refill cycle after it (>= 8 112 draws)."""
-    _roll_past_refills(oracle, 'leduc-holdem', 4096 + 37, 256, 14, flags, 42, past_refills(1))
+    for 28 launches: every env crosses the first refill and one full refill cycle after it (>= 18 096 draws)."""
+    _roll_past_refills(oracle, 'leduc-holdem', 4096 + 37, 256, 28, flags, 42, past_refills(1))
 
 
-@pytest.mark.parametrize('game,T,launches', [('limit-holdem', 128, 6), ('no-limit-holdem', 128, 6),
-                                             ('blackjack', 64, 5)])
+@pytest.mark.parametrize('game,T,launches', [('limit-holdem', 128, 10), ('no-limit-holdem', 128, 10),
+                                             ('blackjack', 64, 9)])
 def test_lane_games_bench_shape_past_refills(oracle, game, T, launches):
     """The other lane-per-env games at their bench T: each env draws ~25-57 words per step, so a few launches
     cross several refills (every slot of the ring is rewritten at least twice)."""
@@ -76,9 +76,9 @@ def test_doudizhu_past_mt_twists(oracle):
 
 
 def test_leduc_full_size_after_precondition(oracle):
-    """The bench's 2^20 Leduc envs after 7 preconditioning launches (T = 256): one timed-shape launch is then
+    """The bench's 2^20 Leduc envs after 14 preconditioning launches (T = 256): one timed-shape launch is then
     compared with the oracle on three windows (start, middle, end) replayed from seeding with the same env ids."""
-    n, T, win, pre = 1 << 20, 256, 256, 7
+    n, T, win, pre = 1 << 20, 256, 256, 14
     v = _vec('leduc-holdem', n, seed=42)
     v.reset()
     out = v.new_traj_out(T)
@@ -105,7 +105,7 @@ def test_cfr_batched_past_refills(oracle):
     per player): tables to 1e-9, RNG positions exactly."""
     from rlcard_amd import VecEnv
     from rlcard_amd.agents import CFRAgent
-    B, K = 256 + 3, 400   # fp64 atomics in any order: 1e-9 holds at this length (800: 1e-8)
+    B, K = 256 + 3, 700
     v = VecEnv('leduc-holdem', B, seed=21)
     agent = CFRAgent(v)
     agent.train(K)
@@ -114,13 +114,15 @@ def test_cfr_batched_past_refills(oracle):
     c = oracle.CFR(keys, lens)
     c.train(K)
     d = np.array([c.draws(i) for i in range(B)])
-    assert d.min() >= v.rng_first_refill + 1000, d.min()   # every stream is past its first refill
+    assert d.min() >= v.rng_first_refill + 300, d.min()   # every stream is past its first refill
     t = c.tables()
     host = agent._tables()
     assert np.array_equal(host['flags'].astype(np.uint8), t['flags'])
     for name, bit in (('policy', 1), ('average_policy', 2), ('regrets', 2)):
         rows = (t['flags'] & bit) != 0
-        np.testing.assert_allclose(host[name][rows], t[name][rows], rtol=1e-9, atol=1e-9 * np.abs(t[name]).max(),
+        # fp64 atomics add the 259 deals of an iteration in any order: the rounding differences grow with the
+        # iterations (1e-9 holds at 400, 9e-9 absolute was seen at 800)
+        np.testing.assert_allclose(host[name][rows], t[name][rows], rtol=1e-7, atol=1e-8 * np.abs(t[name]).max(),
                                    err_msg=name)
     for i in (0, 1, 63, 64, B // 2, B - 1):
         assert v.rng_position(i) == d[i] % v.rng_period

@@ -1,9 +1,9 @@
 #!/bin/bash
-# 8-slot byte ring: the full GPU suite on the new build, then same-box A/B against the HEAD build (4 slots)
+# 8-slot byte ring: the full GPU suite on the new build, then same-box A/B against the previous build
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests/ -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_ring8.log 2>&1 || { tail -40 gpurun_out/gpu_tests_ring8.log; exit 30; }
 tail -2 gpurun_out/gpu_tests_ring8.log
 for g in limit-holdem leduc-holdem blackjack no-limit-holdem; do
-  REPS=2 bash tools/gpu_ab_game.sh $g libcardsim.so libcardsim_head.so || exit 31
+  REPS=2 bash tools/gpu_ab_game.sh $g libcardsim.so libcardsim_ring8.so libcardsim_ring8r.so || exit 31
 done
