@@ -70,12 +70,12 @@ __device__ inline void ring_bytes_serial(const uint32_t* w, uint8_t* ring, uint3
 
 // Philox mode: chunks c0, c0 + step, .. of the next RING_GEN blocks after slot lat (chunk c = 16 bytes: block c / 39,
 // 16-byte piece c % 39), counter (block index wbuf[0] + c / 39, c % 39), key wbuf[1..2]. The caller advances wbuf[0].
-__device__ __forceinline__ void ring_gen_philox(gu32* wbuf, uint32_t lat, int c0, int step)
+__device__ __forceinline__ void ring_gen_philox(gu32* wbuf, uint32_t lat, int c0, int step, int nblk = RING_GEN)
 {
     const uint32_t blk0 = wbuf[0];
     const uint64_t key = (uint64_t)wbuf[1] | (uint64_t)wbuf[2] << 32;
     gu32* ring = wbuf + MT_N;
-    for (int c = c0; c < RING_GEN * PHX_CHUNKS; c += step) {
+    for (int c = c0; c < nblk * PHX_CHUNKS; c += step) {
         const int b = c / PHX_CHUNKS, j = c - b * PHX_CHUNKS;
         uint32_t w[4];
         philox4(key, (uint64_t)(blk0 + (uint32_t)b), (uint64_t)j, w);
@@ -85,7 +85,13 @@ __device__ __forceinline__ void ring_gen_philox(gu32* wbuf, uint32_t lat, int c0
     }
 }
 
-// one lane generates blocks L+1..L+3 after L (slot lat): the rare in-step path and seeding
+// Blocks generated at seeding: env e starts with 1 + e % RING_GEN blocks (slots 0..k-1, latest in slot k-1), so its
+// first refill comes after (k - 1) x 624 draws and the envs' refills -- 15 twists each, all 64 lanes of a wave busy --
+// are spread evenly over the refill cycle instead of all falling in the same launches. The stream is the same
+// (block b always sits in slot b % SLOTS); only when the blocks are generated differs.
+__device__ __forceinline__ uint32_t seed_blocks(int64_t env) { return 1u + (uint32_t)(env % RING_GEN); }
+
+// one lane generates blocks L+1..L+RING_GEN after L (slot lat): the rare in-step path
 __device__ __attribute__((noinline)) void ring_gen_serial(uint32_t* wbuf, uint32_t lat, uint32_t phx = 0)
 {
     if (phx) {

@@ -357,14 +357,16 @@ __global__ __launch_bounds__(BLOCK) void k_seed(uint32_t* mt, uint32_t* ctl, uin
         uint32_t* wbuf = mt + env * RING_ENV_WORDS;
         const int kl = klen[i] == 2 ? 2 : 1;                    // validated on the host; never trust it here
         const uint32_t phx = prm.rng_mode == CS_RNG_PHILOX ? CTL_PHILOX : 0u;
-        if (phx) {   // Philox byte stream: block counter 0, key = the init_by_array key, blocks 0.. into slots 0..
+        const uint32_t kb = seed_blocks(env);                  // blocks 0..kb-1 now (cs_ring.h seed_blocks)
+        if (phx) {   // Philox byte stream: key = the init_by_array key, blocks 0..kb-1 into slots 0..kb-1, counter kb
             wbuf[0] = 0u;
             wbuf[1] = keys[2 * i];
             wbuf[2] = kl == 2 ? keys[2 * i + 1] : 0u;
-            ring_gen_serial(wbuf, SLOT_MASK, phx);
+            ring_gen_philox((gu32*)wbuf, SLOT_MASK, 0, 1, (int)kb);
+            wbuf[0] = kb;
         } else {
             mt_init_by_array(wbuf, keys + 2 * i, kl);
-            for (uint32_t b = 0; b < (uint32_t)RING_GEN; b++) {     // numpy's first draws: block 0 = twist(S0)
+            for (uint32_t b = 0; b < kb; b++) {     // numpy's first draws: block 0 = twist(S0)
                 mt_twist_inplace(wbuf);
                 ring_bytes_serial(wbuf, (uint8_t*)(wbuf + MT_N), b);
             }
@@ -374,7 +376,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed(uint32_t* mt, uint32_t* ctl, uin
         g.blank();
         g.store(st, n, env);
         if constexpr (DqOf<G>::value > 0) st[(int64_t)G::GW * n + env] = 0u;   // empty deal queue
-        ctl[env] = 0u | (uint32_t)(RING_GEN - 1) << CTL_LAT_SHIFT | phx;   // position 0, latest block in slot RING_GEN-1
+        ctl[env] = 0u | (kb - 1u) << CTL_LAT_SHIFT | phx;   // position 0, latest block in slot kb - 1
         return;
     }
     MtLane m;
