@@ -31,23 +31,18 @@ MT_N = 624              # words per MT19937 block
 
 # per game: default envs per GPU (BASELINE.json configs), default fused steps per launch, packed state bytes per env
 # read + written once per launch (state words + the RNG control word), the expected tempered-u32 MT19937 draws per
-# env-step under random play (exact acceptance rates of random_interval x random-play game lengths), and
-# the stream geometry: draws before the first block refill and draws per refill. Lane-per-env games keep a byte ring
-# of RING_SLOTS = 16 blocks (cs_engine.h CS_RING_SLOTS), 15 generated at seeding and 15 more per refill once the lane
-# is inside the last one (cs_ring.h: needs_refill at position >= 14 x 624); DouDizhu a two-block word window that twists
-# one block per 624 draws (cs_doudizhu.hip WaveMt::window, first twist ~1 184 draws in).
+# env-step under random play (exact acceptance rates of random_interval x random-play game lengths). The
+# stream geometry (draws before the first refill, draws per refill) comes from the built library (VecEnv.rng_period:
+# the byte ring's CS_RING_SLOTS, or DouDizhu's two-block word window), see precondition_launches.
 # Fused steps per launch, measured on one box: Leduc 256 vs 128 +3 % (T >= 256), 512 vs 256 -9 %;
 # Limit / No-limit 256 vs 128 +1.5 / +2 % (128 vs 64 +2.5 / +3 %), DouDizhu 128 vs 64 -7 %.
-RING_SLOTS = 16
-RING = dict(first_refill=(RING_SLOTS - 2) * MT_N, per_refill=(RING_SLOTS - 1) * MT_N)
 GAMES = {
-    'leduc-holdem': dict(envs=1 << 20, T=256, state_bytes=2 * 4 + 4, draws_per_step=2.83, **RING),
-    'limit-holdem': dict(envs=262144, T=256, state_bytes=12 * 4 + 4, draws_per_step=24.5, **RING),
-    'blackjack': dict(envs=1 << 20, T=64, state_bytes=20 * 4 + 4, draws_per_step=57.0, **RING),
-    'doudizhu': dict(envs=65536, T=64, state_bytes=20 * 4 + 4, draws_per_step=1.21, first_refill=1184,
-                     per_refill=MT_N),
+    'leduc-holdem': dict(envs=1 << 20, T=256, state_bytes=2 * 4 + 4, draws_per_step=2.83),
+    'limit-holdem': dict(envs=262144, T=256, state_bytes=12 * 4 + 4, draws_per_step=24.5),
+    'blackjack': dict(envs=1 << 20, T=64, state_bytes=20 * 4 + 4, draws_per_step=57.0),
+    'doudizhu': dict(envs=65536, T=64, state_bytes=36 * 4 + 4, draws_per_step=1.21),
     # not a BASELINE config; draws/step counted on the oracle (4096 envs x 256 random steps)
-    'no-limit-holdem': dict(envs=262144, T=256, state_bytes=4 * 4 + 4, draws_per_step=26.3, **RING),
+    'no-limit-holdem': dict(envs=262144, T=256, state_bytes=4 * 4 + 4, draws_per_step=26.3),
 }
 TIMED_TARGET_S = 2.0     # default --steps: enough launches for >= ~2 s of timed region (box variance, SMI sampler)
 
@@ -66,11 +61,12 @@ def alg_bytes_philox(info, T, game):
     return alg_bytes_per_env_step(info, T, game) - 8.0 * GAMES[game]['draws_per_step']
 
 
-def precondition_launches(game, T):
+def precondition_launches(game, T, vec):
     """Untimed launches so that the timed ones run at the steady-state refill rate: a freshly seeded stream refills
-    nothing for its first `first_refill` draws; run until the average env has also passed two refills."""
+    nothing for its first draws (VecEnv.rng_first_refill, the worst case over envs); run until the average env has
+    also passed two refills (VecEnv.rng_per_refill), the geometry of the library actually built."""
     g = GAMES[game]
-    return int(math.ceil((g['first_refill'] + 2 * g['per_refill']) / (g['draws_per_step'] * T)))
+    return int(math.ceil((vec.rng_first_refill + 2 * vec.rng_per_refill) / (g['draws_per_step'] * T)))
 
 
 def kernel_source_digest():
@@ -215,7 +211,7 @@ def main():
 
     stream = torch.cuda.current_stream()
     t_launch = 0
-    pre = precondition_launches(game, T) if args.precondition else 0
+    pre = precondition_launches(game, T, env) if args.precondition else 0
     for w in range(pre):
         env.rollout(T, policy_seed=5, t0=t_launch * T, out=traj)
         t_launch += 1

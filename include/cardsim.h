@@ -201,7 +201,9 @@ int cs_dmc_fill(cs_dmc* d, int32_t T_roll, const cs_traj_out* traj, int64_t* rea
 /* get_batch: `count` chunk ids (DEVICE int64, all of player `player`) stacked along dim 1 into `out`. */
 int cs_dmc_gather(cs_dmc* d, int32_t player, const int64_t* chunks, int64_t count, const cs_dmc_batch* out,
                   void* stream);
-/* Synchronous: bit 0 = rows were dropped because a stream's ring was full (slots too few, or chunks not gathered). */
+/* Synchronous, sticky flags: bit 0 = rows were dropped because a stream's ring was full (slots too few, or chunks not
+ * gathered) -- those streams are broken (no chunk holding a dropped row is ever listed, later rows of the stream are
+ * dropped too); bit 1 = a fill had more ready chunks than `cap` (the rest are listed by the next fill). */
 int cs_dmc_status(cs_dmc* d, uint32_t* host_flags);
 
 /* DMCNet scoring of legal actions (model.py:21-43 forward, 91-110 predict), first layer fused: for entry i (state

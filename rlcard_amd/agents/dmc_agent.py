@@ -173,7 +173,11 @@ class ActorBuffers:
             _abi.check(_abi.lib().cs_dmc_fill(self._d, int(T), C.byref(s), _ptr(self._ready), self.cap,
                                               _ptr(self._nready), self.vec._stream()), 'cs_dmc_fill')
         n = int(self._nready.item())
-        return self._ready[:min(n, self.cap)].clone()
+        if self.dropped():
+            raise _abi.CardsimError('DMC actor buffers overflowed: a (env, player) ring of %d chunks was full, rows were '
+                                    'dropped (gather the ready chunks before the next fill, or use more slots)'
+                                    % self.slots)
+        return self._ready[:n].clone()
 
     def player_of(self, chunks):
         return (chunks // self.slots) % self.vec.num_players

@@ -23,6 +23,7 @@ struct cs_handle {
     cs::ddz::Tab tab;    // doudizhu: views into it, passed to the kernels by value
     void* scan_tmp;      // cs_legal_lists: prefix-scan scratch, grown on demand
     size_t scan_bytes;
+    cs::CfrScratch cfr;  // cs_cfr_train with n > 1: the ordered reduction's records and sort buffers
 };
 
 namespace {
@@ -135,6 +136,7 @@ void cs_destroy(cs_handle* h)
     if (h->b.sbuf) (void)hipFree(h->b.sbuf);
     if (h->table_dev) (void)hipFree(h->table_dev);
     if (h->scan_tmp) (void)hipFree(h->scan_tmp);
+    if (h->cfr.mem) (void)hipFree(h->cfr.mem);
     delete h;
 }
 
@@ -225,7 +227,7 @@ int cs_cfr_train(cs_handle* h, int32_t iterations, int64_t iteration0, double* p
     int r = set_device(h);
     if (r != CS_OK) return r;
     const cs::CfrTables t{policy, average_policy, regrets, flags};
-    hipError_t e = cs::launch_cfr(h->b, iterations, iteration0, t, (hipStream_t)stream);
+    hipError_t e = cs::launch_cfr(h->b, iterations, iteration0, t, &h->cfr, (hipStream_t)stream);
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_cfr_train");
 }
 

@@ -10,8 +10,14 @@
 //   ((hand * 4 + public + 1 (0 = none)) * 15 + my chips) * 15 + others' chips
 // flags[CFR_NI] u32: bit 0 = key present in policy, bit 1 = key present in regrets / average_policy.
 // Every fp64 operation follows the reference's order and nothing is contracted into FMAs, so one env (one deal per
-// player per iteration, the reference agent) is bit-exact; with more envs the table updates are fp64 atomics
-// (summation order varies run to run).
+// player per iteration, the reference agent) is bit-exact.
+// Batched mode (n envs, one deal each per player per iteration; oracle/or_cfr.c): the table sums must come out in one
+// fixed order -- per iteration, player 0's pass then player 1's, envs ascending, each deal's nodes in traversal
+// (post-)order, as the oracle adds them. Each lane writes its deal's contributions as records (infoset | legal bits
+// key, regret and average-policy terms) at (pass, env, node) slots; a stable radix sort on the 12-bit infoset groups
+// them per infoset keeping that order, and one thread per (infoset, action) adds its segment sequentially. Same
+// bits every run, equal to the oracle's at any iteration count.
+#include <hipcub/hipcub.hpp>
 #include "cs_device.h"
 #include "cs_ring.h"
 #include "cs_engine.h"
@@ -25,6 +31,18 @@ namespace {
 
 constexpr int NA = 4;
 constexpr int MAXD = 12;   // deepest Leduc betting line: 8 actions (two raises per round) + root
+// records per (pass, env): the traversing player's decision nodes of one deal's betting tree -- 18 for either seat
+// (the tree's shape does not depend on the cards); slots past the node count hold REC_NONE keys
+constexpr int REC_CAP = 24;
+constexpr uint32_t REC_NONE = 0xFFFu;   // sorts after every infoset (< 2700)
+
+// batched-mode record buffers: key u16 (infoset | legal << 12), the regret and average-policy terms of the 4 actions
+struct Recs {
+    uint16_t* key;
+    double* val;      // [slot][8]: regret[4], avg[4]
+    int64_t n;        // envs
+    int pass;
+};
 
 struct Frame {
     uint32_t w[2];        // packed Leduc state (Leduc::store with n = 1)
@@ -40,12 +58,6 @@ __device__ __forceinline__ int leduc_infoset(const Leduc& g, int p)
     const int hand = (p ? g.h1 : g.h0) >> 1, pub = g.rc >= 1 ? (g.pub >> 1) + 1 : 0;
     const int my = p ? g.in1 : g.in0, op = g.in0 + g.in1 - my;
     return ((hand * 4 + pub) * 15 + my) * 15 + op;
-}
-
-__device__ __forceinline__ void add_f64(double* p, double v, bool atomic)
-{
-    if (atomic) atomicAdd(p, v);
-    else *p = *p + v;
 }
 
 // traverse_tree entry for a non-terminal node: acting player, infoset, legal ids, remove_illegal(policy row)
@@ -91,30 +103,46 @@ __device__ __forceinline__ void deliver(Frame& f, int a, double u0, double u1)
     f.au[a] = f.cp ? u1 : u0;
 }
 
-// cfr_agent.py:84-97: regrets and average policy at the traversing player's node
-__device__ __forceinline__ void record(const Frame& f, double iteration, const CfrTables& t, bool atomic)
+// cfr_agent.py:84-97: regrets and average policy at the traversing player's node; batched mode writes the terms as
+// the lane's next record instead of adding them
+__device__ __forceinline__ void record(const Frame& f, double iteration, const CfrTables& t, const Recs& rc,
+                                       bool batched, int64_t slot)
 {
     const double pp = f.cp ? f.pr1 : f.pr0;
     const double cf = f.cp == 0 ? 1.0 * f.pr1 : f.pr0 * 1.0;
     const double us = f.cp ? f.su1 : f.su0;
     if (!(t.flags[f.idx] & 2u)) atomicOr(&t.flags[f.idx], 2u);
+    if (batched) {
+        double* v = rc.val + slot * 8;
+#pragma unroll
+        for (int a = 0; a < NA; a++) {
+            const bool l = (f.legal >> a) & 1u;
+            v[a] = l ? cf * (f.au[a] - us) : 0.0;
+            v[NA + a] = l ? (iteration * pp) * f.ap[a] : 0.0;
+        }
+        rc.key[slot] = (uint16_t)(f.idx | (f.legal << 12));
+        return;
+    }
 #pragma unroll
     for (int a = 0; a < NA; a++) {
         if (!((f.legal >> a) & 1u)) continue;
         const double regret = cf * (f.au[a] - us);
-        add_f64(&t.regrets[f.idx * NA + a], regret, atomic);
-        add_f64(&t.avg[f.idx * NA + a], (iteration * pp) * f.ap[a], atomic);
+        t.regrets[f.idx * NA + a] = t.regrets[f.idx * NA + a] + regret;
+        t.avg[f.idx * NA + a] = t.avg[f.idx * NA + a] + (iteration * pp) * f.ap[a];
     }
 }
 
-// the whole tree under the lane's current deal, for traversing player `player`
-__device__ void traverse(const Leduc& root, int player, double iteration, const CfrTables& t, bool atomic)
+// the whole tree under the lane's current deal, for traversing player `player` (rc: batched mode, the lane's
+// records start at slot0)
+__device__ void traverse(const Leduc& root, int player, double iteration, const CfrTables& t, const Recs& rc,
+                         bool batched, int64_t slot0)
 {
     Frame S[MAXD];
     int d = 0;
+    int nrec = 0;
     enter(S[0], root, 1.0, 1.0, t);
     RingLane<> none;   // Leduc::step draws nothing
-    none.init(nullptr, 2u << 12);
+    none.init(nullptr, CTL_IDLE);
     while (true) {
         Frame& f = S[d];
         const uint32_t rem = f.legal & ~((1u << f.next) - 1u);
@@ -136,32 +164,34 @@ __device__ void traverse(const Leduc& root, int player, double iteration, const 
                 enter(S[d], c, p0, p1, t);
             }
         } else {
-            if ((int)f.cp == player) record(f, iteration, t, atomic);
+            if ((int)f.cp == player && nrec < REC_CAP) record(f, iteration, t, rc, batched, slot0 + nrec++);
             const double u0 = f.su0, u1 = f.su1;
             if (d == 0) break;
             d--;
             deliver(S[d], (int)S[d].next - 1, u0, u1);
         }
     }
+    if (batched)
+        for (int k = nrec; k < REC_CAP; k++) rc.key[slot0 + k] = (uint16_t)REC_NONE;
 }
 
 __global__ __launch_bounds__(256) void k_cfr_iteration(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
-                                                       CfrTables t, double iteration)
+                                                       CfrTables t, double iteration, Recs recs)
 {
     const int lane = threadIdx.x & (WAVE - 1);
     const int64_t env = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = env < n;
-    const bool atomic = n > 1;
+    const bool batched = n > 1;
     RingLane<> m;
     if (valid) m.init(mt + env * RING_ENV_WORDS, ctl[env]);
-    else m.init(mt, 2u << 12);   // never needs a refill
+    else m.init(mt, CTL_IDLE);   // never needs a refill
     Leduc g;
     g.blank();
     if (valid) g.load(st, n, env);
     for (int p = 0; p < 2; p++) {
         if (valid) g.reset(m);          // env.reset(): a new deal from the env's own stream
         ring_refill_wave(m, lane);      // all 64 lanes
-        if (valid) traverse(g, p, iteration, t, atomic);
+        if (valid) traverse(g, p, iteration, t, recs, batched, ((int64_t)p * n + env) * REC_CAP);
     }
     if (valid) {
         g.store(st, n, env);            // the env is left at the last deal's root (every step stepped back)
@@ -192,17 +222,102 @@ __global__ void k_cfr_update(CfrTables t)
     t.flags[i] |= 1u;
 }
 
+__global__ void k_iota(uint32_t* v, int64_t m)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) v[i] = (uint32_t)i;
+}
+
+// segment [seg[2 k], seg[2 k + 1]) of the sorted keys holds infoset k's records (empty segments stay 0, 0)
+__global__ void k_cfr_segments(const uint16_t* __restrict__ key, int64_t m, int32_t* seg)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t k = key[i] & 0xFFFu, kp = i > 0 ? key[i - 1] & 0xFFFu : 0xFFFFu;
+    const uint32_t kn = i + 1 < m ? key[i + 1] & 0xFFFu : 0xFFFFu;
+    if (k >= (uint32_t)CFR_NI) return;
+    if (k != kp) seg[2 * k] = (int32_t)i;
+    if (k != kn) seg[2 * k + 1] = (int32_t)i + 1;
+}
+
+// one thread per (infoset, action): its records in (pass, env, node) order, added one by one as the oracle does
+__global__ void k_cfr_reduce(const uint16_t* __restrict__ key, const uint32_t* __restrict__ slot,
+                             const double* __restrict__ val, const int32_t* __restrict__ seg, CfrTables t)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= CFR_NI * NA) return;
+    const int idx = i / NA, a = i % NA;
+    const int32_t lo = seg[2 * idx], hi = seg[2 * idx + 1];
+    if (lo >= hi) return;
+    double r = t.regrets[i], v = t.avg[i];
+    for (int32_t j = lo; j < hi; j++) {
+        if (!((key[j] >> (12 + a)) & 1u)) continue;
+        const double* x = val + (int64_t)slot[j] * 8;
+        r = r + x[a];
+        v = v + x[NA + a];
+    }
+    t.regrets[i] = r;
+    t.avg[i] = v;
+}
+
+size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
 }  // namespace
 
-hipError_t launch_cfr(const Buffers& b, int32_t iterations, int64_t iteration0, const CfrTables& t, hipStream_t s)
+hipError_t launch_cfr(const Buffers& b, int32_t iterations, int64_t iteration0, const CfrTables& t, CfrScratch* sc,
+                      hipStream_t s)
 {
     const dim3 grid((unsigned)((b.n + 255) / 256)), ugrid((CFR_NI + 255) / 256);
+    Recs recs{nullptr, nullptr, b.n, 0};
+    uint16_t *key_out = nullptr;
+    uint32_t *slot_in = nullptr, *slot_out = nullptr;
+    int32_t* seg = nullptr;
+    void* sort_tmp = nullptr;
+    size_t sort_bytes = 0;
+    const int64_t m = 2 * b.n * REC_CAP;   // records per iteration
+    hipError_t e;
+    if (b.n > 1) {
+        if (m > (int64_t)INT32_MAX) return hipErrorInvalidValue;
+        e = hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (const uint16_t*)nullptr, (uint16_t*)nullptr,
+                                               (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)m, 0, 12, s);
+        if (e != hipSuccess) return e;
+        const size_t o_val = 0, o_key = al256(o_val + (size_t)m * 64), o_kout = al256(o_key + (size_t)m * 2),
+                     o_sin = al256(o_kout + (size_t)m * 2), o_sout = al256(o_sin + (size_t)m * 4),
+                     o_seg = al256(o_sout + (size_t)m * 4), o_tmp = al256(o_seg + (size_t)CFR_NI * 8),
+                     total = o_tmp + sort_bytes;
+        const bool fresh = sc->bytes < total;
+        if (fresh) {
+            if (sc->mem) (void)hipFree(sc->mem);
+            sc->mem = nullptr;
+            sc->bytes = 0;
+            if ((e = hipMalloc(&sc->mem, total)) != hipSuccess) return e;
+            sc->bytes = total;
+        }
+        uint8_t* base = (uint8_t*)sc->mem;
+        recs.val = (double*)(base + o_val);
+        recs.key = (uint16_t*)(base + o_key);
+        key_out = (uint16_t*)(base + o_kout);
+        slot_in = (uint32_t*)(base + o_sin);
+        slot_out = (uint32_t*)(base + o_sout);
+        seg = (int32_t*)(base + o_seg);
+        sort_tmp = base + o_tmp;
+        hipLaunchKernelGGL(k_iota, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, slot_in, m);
+    }
     for (int32_t it = 0; it < iterations; it++) {
         hipLaunchKernelGGL(k_cfr_iteration, grid, dim3(256), 0, s, b.mt, b.ctl, b.state, b.n, t,
-                           (double)(iteration0 + it + 1));
+                           (double)(iteration0 + it + 1), recs);
+        if (b.n > 1) {
+            if ((e = hipMemsetAsync(seg, 0, (size_t)CFR_NI * 8, s)) != hipSuccess) return e;
+            size_t tb = sort_bytes;
+            e = hipcub::DeviceRadixSort::SortPairs(sort_tmp, tb, (const uint16_t*)recs.key, key_out,
+                                                   (const uint32_t*)slot_in, slot_out, (int)m, 0, 12, s);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(k_cfr_segments, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, key_out, m, seg);
+            hipLaunchKernelGGL(k_cfr_reduce, dim3((CFR_NI * NA + 63) / 64), dim3(64), 0, s, key_out, slot_out,
+                               recs.val, seg, t);
+        }
         hipLaunchKernelGGL(k_cfr_update, ugrid, dim3(256), 0, s, t);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
+        if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
 }

@@ -35,7 +35,7 @@ std::string table_build_host(std::vector<uint8_t>& host, size_t off[4], Tab* tab
     uint32_t na, pass;
     memcpy(&na, cs_ddz_blob + 4, 4);
     memcpy(&pass, cs_ddz_blob + 8, 4);
-    if (na != (uint32_t)NA || pass != (uint32_t)PASS || size != 16 + (size_t)na * 10)
+    if (na != (uint32_t)NA || pass != (uint32_t)PASS || size != 16 + (size_t)na * 12)   // + the host-only tc_order
         return "doudizhu action table has an unexpected size";
     std::vector<uint64_t> cnt(NA);
     memcpy(cnt.data(), cs_ddz_blob + 16, (size_t)NA * 8);

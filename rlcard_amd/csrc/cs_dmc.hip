@@ -52,7 +52,9 @@ __global__ __launch_bounds__(DBLOCK) void k_dmc_index(const uint8_t* __restrict_
             continue;
         }
         const int64_t s = e * P + p, w = ctr[s];
-        if (w - emitted[s] * Tc >= (int64_t)R * Tc) {   // would overwrite a chunk not yet handed out: drop
+        if (w - emitted[s] * Tc >= (int64_t)R * Tc) {
+            // would overwrite a chunk not yet handed out: the row is dropped and not counted (ctr stays), so no chunk
+            // holding it is ever listed as ready; the stream is broken from here on and the host raises (flag bit 0)
             dst[row] = -1;
             atomicOr(flag, 1u);
         } else {
@@ -61,14 +63,13 @@ __global__ __launch_bounds__(DBLOCK) void k_dmc_index(const uint8_t* __restrict_
             tgt[r] = nan;   // filled when the game ends
             ret[r] = 0.f;
             dne[r] = 0;
+            ctr[s] = w + 1;
         }
-        ctr[s] = w + 1;
         if (done[row]) {   // the game's rows of every player get its payoff (utils.py:121-128)
             for (int q = 0; q < P; q++) {
                 const int64_t sq = e * P + q, end = ctr[sq];
                 const float pay = reward[row * P + q];
-                for (int64_t i = gstart[sq]; i < end; i++) {
-                    if (i - emitted[sq] * Tc >= (int64_t)R * Tc) continue;   // dropped above
+                for (int64_t i = gstart[sq]; i < end; i++) {   // rows [gstart, ctr) are all in the ring
                     const int64_t r = ring_row(sq, i, Tc, R);
                     tgt[r] = pay;
                     if (i == end - 1) {
@@ -87,18 +88,25 @@ __global__ __launch_bounds__(DBLOCK) void k_dmc_index(const uint8_t* __restrict_
     }
 }
 
-// ready chunk ids (stream s, chunk k -> s * R + k % R) in (env, player, chunk) order; emitted advances
+// ready chunk ids (stream s, chunk k -> s * R + k % R) in (env, player, chunk) order; emitted advances by the ids
+// actually listed: chunks past `cap` stay queued for the next fill (flag bit 1)
 __global__ __launch_bounds__(DBLOCK) void k_dmc_ready(const int32_t* __restrict__ counts,
                                                       const int64_t* __restrict__ offsets, int64_t streams, int R,
-                                                      int64_t* emitted, int64_t* ready, int64_t cap, int64_t* nready)
+                                                      int64_t* emitted, int64_t* ready, int64_t cap, int64_t* nready,
+                                                      uint32_t* flag)
 {
     const int64_t s = (int64_t)blockIdx.x * DBLOCK + threadIdx.x;
-    if (s == 0) *nready = offsets[streams];
+    if (s == 0) {
+        const int64_t total = offsets[streams];
+        *nready = total < cap ? total : cap;
+        if (total > cap) atomicOr(flag, 2u);
+    }
     if (s >= streams) return;
-    const int c = counts[s];
-    const int64_t k0 = emitted[s], o = offsets[s];
-    for (int i = 0; i < c; i++)
-        if (o + i < cap) ready[o + i] = s * R + (k0 + i) % R;
+    const int64_t o = offsets[s];
+    const int64_t room = cap - o;
+    const int c = room <= 0 ? 0 : (counts[s] < room ? counts[s] : (int)room);
+    const int64_t k0 = emitted[s];
+    for (int i = 0; i < c; i++) ready[o + i] = s * R + (k0 + i) % R;
     emitted[s] = k0 + c;
 }
 
@@ -186,7 +194,7 @@ hipError_t launch_dmc_fill(const Buffers& b, const DmcRing& d, int32_t T, const 
     e = hipcub::DeviceScan::ExclusiveSum(*tmp, need, d.counts, d.offsets, streams + 1, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_dmc_ready, dim3((unsigned)((streams + DBLOCK - 1) / DBLOCK)), dim3(DBLOCK), 0, s, d.counts,
-                       d.offsets, streams, d.slots, d.emitted, ready, cap, nready);
+                       d.offsets, streams, d.slots, d.emitted, ready, cap, nready, d.flag);
     if (tr.obs) {
         const int64_t work = rows * ((b.obs_dim + 3) / 4);
         hipLaunchKernelGGL(k_dmc_rows, dim3((unsigned)((work + DBLOCK - 1) / DBLOCK)), dim3(DBLOCK), 0, s,

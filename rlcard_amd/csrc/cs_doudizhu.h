@@ -23,7 +23,7 @@ constexpr int OBS = 901;          // peasant obs; the landlord's 790 are zero-pa
 constexpr int OBS_LANDLORD = 790;
 constexpr int LB = (NA + 7) / 8;  // 3 434 legal bytes per row
 constexpr int P = 3;
-constexpr int WORDS = 20;         // packed state words per env (env-major rows, see below)
+constexpr int WORDS = 36;         // packed state words per env (env-major 144-B rows, see below)
 constexpr int MAX_GROUPS = 320;   // (type, weight) groups: 308 in the reference table, scanned 64 per wave pass
 constexpr int TYPE_BOMB = 35, TYPE_ROCKET = 36;  // indices in tools/gen_ddz_table.py TYPE_NAMES
 constexpr uint32_t NONE = 3;      // "no player" for greater_player / winner
@@ -56,7 +56,12 @@ struct Tab {
 //   17     number of trace entries (game.py:65 round.trace)
 //   18     greater_player | greater_player's last play id << 16   (player.py:60-108, round.py:54-65)
 //   19     current player | winner << 8                            (game.py:66-81; winner NONE = not over)
-enum { W_HAND = 0, W_PLAYED = 6, W_HIST = 12, W_NTRACE = 17, W_GREATER = 18, W_CUR = 19 };
+//   20..33 the dealt deck: byte k = the card at shuffled position k (sorted-deck id: rank * 4 + suit S H D C for
+//          rank < 13, 52 black joker, 53 red joker; dealer.py:12-76). Written at the deal, read by the host only:
+//          the suit-level hands and seen_cards of raw_obs / get_perfect_information (player.py:46-58, round.py:25-39)
+//   34, 35 zero (16-B rows)
+enum { W_HAND = 0, W_PLAYED = 6, W_HIST = 12, W_NTRACE = 17, W_GREATER = 18, W_CUR = 19, W_DECK = 20 };
+constexpr int DECK_BYTES = 4 * (WORDS - W_DECK);   // 64: bytes 54..63 zero
 
 // The state k_seed writes (lane per env, like every other game): a finished game (winner 0), so the next
 // reset/step deals.

@@ -99,6 +99,7 @@ struct Env {
     uint32_t ggrp;              // (type, weight) group of gplay (kept in the spare high half of state word 16)
     uint64_t hcnt;              // PER LANE: lane s = 3..11 holds the packed counts of hist(s - 3) (0: pass / none),
                                 // shifted down one lane per action, so observations never reload the action table
+    uint32_t deck;              // PER LANE: lane k < 54 holds the card dealt at shuffled position k (state W_DECK)
 
     __device__ __forceinline__ uint32_t hist(uint32_t k) const   // k may differ per lane
     {
@@ -142,6 +143,7 @@ struct Env {
         gplay = g >> 16;
         cur = c & 0xFFu;
         winner = (c >> 8) & 0xFFu;
+        deck = lane < 54 ? (uint32_t)((const uint8_t*)(st + env * WORDS + W_DECK))[lane] : 0u;
     }
     __device__ __forceinline__ void store(uint32_t* st, int64_t env, int lane) const
     {
@@ -153,6 +155,7 @@ struct Env {
             o[3] = make_uint4(hw0, hw1, hw2, hw3);
             o[4] = make_uint4((hw4 & 0xFFFFu) | (ggrp << 16), ntrace, greater | (gplay << 16), cur | (winner << 8));
         }
+        ((uint8_t*)(st + env * WORDS + W_DECK))[lane] = (uint8_t)(lane < 54 ? deck : 0u);   // one 64-B segment
     }
 
     // Player.play + Round.proceed_round + Game.step (player.py:88-108, round.py:54-79, game.py:55-81)
@@ -328,6 +331,7 @@ __device__ __forceinline__ void deal(Env& e, M& m, int lane)
         h2 |= (uint64_t)__popcll(b & own2) << (4 * r);
     }
     e.h0 = h0; e.h1 = h1; e.h2 = h2;
+    e.deck = deck;
     e.q0 = e.q1 = e.q2 = 0;
     e.hw0 = e.hw1 = e.hw2 = e.hw3 = e.hw4 = 0xFFFFFFFFu;
     e.ggrp = 0;
@@ -837,6 +841,7 @@ __global__ __launch_bounds__(BLOCK) void k_debug_legal(const uint8_t* __restrict
     e.hw0 = e.hw1 = e.hw2 = e.hw3 = e.hw4 = 0xFFFFFFFFu;
     e.ntrace = 0;
     e.hcnt = 0;
+    e.deck = 0;
     e.cur = 0;
     e.winner = NONE;
     const bool lead = pv < 0 || pv >= PASS;

@@ -113,7 +113,13 @@ struct CfrTables {
     double* regrets;
     uint32_t* flags;
 };
-hipError_t launch_cfr(const Buffers& b, int32_t iterations, int64_t iteration0, const CfrTables& t, hipStream_t s);
+// batched mode (n > 1): the deals' table contributions, reduced in a fixed order (cs_cfr.hip); handle-owned
+struct CfrScratch {
+    void* mem;      // one allocation, grown on demand
+    size_t bytes;
+};
+hipError_t launch_cfr(const Buffers& b, int32_t iterations, int64_t iteration0, const CfrTables& t, CfrScratch* sc,
+                      hipStream_t s);
 
 // cs_traj.hip
 hipError_t launch_transitions(const Buffers& b, int32_t T, const cs_traj_out& tr, const cs_trans_out& o,

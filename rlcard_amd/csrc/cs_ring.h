@@ -42,6 +42,9 @@ constexpr uint32_t CTL_POS_MASK = 0x3FFFu;   // ctl bits 0..13: ring position
 constexpr int CTL_LAT_SHIFT = 19;            // ctl bits 19..22: slot of the latest block (16..18: flags)
 constexpr uint32_t CTL_PHILOX = 1u << 18;       // ctl bit: the env's stream is the Philox byte stream
 constexpr int PHX_CHUNKS = MT_N / 16;           // 39 Philox blocks (16 bytes) per ring block
+// ctl word of a lane that holds no env (tail lanes of a wave): position 0 inside the latest block, so it never
+// reaches a refill (cs_skeleton.h ring_lane, cs_cfr.hip)
+constexpr uint32_t CTL_IDLE = (uint32_t)(RING_GEN - 1) << CTL_LAT_SHIFT;
 
 __device__ __forceinline__ uint32_t shfl(uint32_t v, int src_lane)
 {

@@ -73,7 +73,7 @@ __device__ __forceinline__ RingLane<MODE> ring_lane(uint32_t* mt, const uint32_t
 {
     RingLane<MODE> m;
     if (c.valid) m.init(mt + c.env * RING_ENV_WORDS, ctl[c.env]);
-    else m.init(mt, 0u | (uint32_t)(RING_GEN - 1) << CTL_LAT_SHIFT);
+    else m.init(mt, CTL_IDLE);
     return m;
 }
 

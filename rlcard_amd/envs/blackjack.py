@@ -28,10 +28,17 @@ class BlackjackEnv(Env):
             hands.append([card_str((w[15 + (12 * h + k) // 4] >> (8 * ((12 * h + k) % 4))) & 255) for k in range(n)])
         return hands
 
-    def _raw_obs(self, player_id, legal):
+    def _raw_obs(self, player_id, legal, via):
+        """Game.get_state (games/blackjack/game.py:162-190) -- or, for the state Env.step returns, the dict Game.step
+        builds (game.py:104-117): the same entries, 'actions' moved after the hands."""
         hands = self._hands()
         dealer = hands[-1] if self.is_over() else hands[-1][1:]
-        return {'actions': tuple(self.actions), 'state': (hands[player_id], dealer)}
+        seats = [('player%d hand' % i, hands[i]) for i in range(self.num_players)]
+        if via == 'step':
+            items = seats + [('dealer hand', dealer), ('actions', tuple(self.actions))]
+        else:
+            items = [('actions', tuple(self.actions))] + seats + [('dealer hand', dealer)]
+        return dict(items + [('state', (hands[player_id], dealer))])
 
     def _payoff_array(self, r):
         return np.asarray(r, dtype=np.int64)        # blackjack.py get_payoffs: 1 win, 0 tie, -1 loss

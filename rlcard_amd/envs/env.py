@@ -79,6 +79,7 @@ class _Io:
                                 C.c_void_p(base + self.o_done))
         self.obs_out = _abi.StepOut(self.out.obs, self.out.legal, self.out.player, None, self.out.done)
         self.ids_base = self.ids.data_ptr()
+        self.vec = vec   # the record stays registered on vec's handle until close()
         _abi.check(_abi.lib().cs_set_step_record(vec._h, 0, C.c_void_p(base + self.o_words), C.c_void_p(base)),
                    'cs_set_step_record')
         self.expect = 0
@@ -103,6 +104,10 @@ class _Io:
 
     def close(self):
         if getattr(self, '_hp', None) is not None and self._hp.value:
+            vec = getattr(self, 'vec', None)
+            if vec is not None and vec._h is not None:   # unregister first: later kernels must not write freed memory
+                torch.cuda.synchronize(vec.device)
+                _abi.lib().cs_set_step_record(vec._h, 0, None, None)
             _hip_lib().hipHostFree(self._hp)
             self._hp = None
 
@@ -170,7 +175,8 @@ class Env(object):
         self._payoffs = None
         self._history = []
         self._last = out
-        return self._extract_state(out, out['player']), out['player']
+        self._after_deal()
+        return self._extract_state(out, out['player'], 'reset'), out['player']
 
     def step(self, action, raw_action=False):
         if self._last is None:
@@ -182,12 +188,19 @@ class Env(object):
         if self.allow_step_back:
             self._history.append((self._state_words(), dict(self._last), self._payoffs))
         self.timestep += 1
-        self.action_recorder.append((self.get_player_id(), decoded))
+        player = self.get_player_id()
+        self.action_recorder.append((player, decoded))
+        was_over = bool(self._last['done'])
         out = self._call('step', self._action_id(decoded))
         if out['done']:
             self._payoffs = out['reward']
         self._last = out
-        return self._extract_state(out, out['player']), out['player']
+        if was_over:        # lazy auto-reset: the engine dealt a new game instead (include/cardsim.h cs_step)
+            self._payoffs = None
+            self._after_deal()
+        else:
+            self._after_step(player, decoded)
+        return self._extract_state(out, out['player'], 'step'), out['player']
 
     def step_back(self):
         """env.py:88-108: restore the game as it was before the last step (the packed state words, written back
@@ -204,6 +217,7 @@ class Env(object):
         self._vec.set_env_state_words(0, words)
         self._words = list(words)
         self._last, self._payoffs = last, payoffs
+        self._after_step_back()
         player_id = self.get_player_id()
         return self.get_state(player_id), player_id
 
@@ -275,16 +289,32 @@ class Env(object):
             return list(_BYTE_IDS[int(lg[0])])
         return legal_ids(lg)
 
-    def _extract_state(self, out, player_id):
-        ids = self._legal_ids(out)
+    def _extract_state(self, out, player_id, via='get_state'):
+        """via: 'reset', 'step' or 'get_state' -- the Game method whose state dict the reference's raw_obs is (their
+        key orders differ for Blackjack, games/blackjack/game.py:104-117 vs 162-190)."""
+        ids = self._legal_order(out)
         state = {
             'legal_actions': OrderedDict((i, self._legal_value(i)) for i in ids),
             'obs': self._obs_of(out['obs'], player_id),
-            'raw_obs': self._raw_obs(player_id, ids),
+            'raw_obs': self._raw_obs(player_id, ids, via),
             'raw_legal_actions': [self._raw_action(i) for i in ids],
             'action_record': self.action_recorder,
         }
         return state
+
+    def _legal_order(self, out):
+        """The legal ids in the order the reference lists them (ascending for every game but DouDizhu)."""
+        return self._legal_ids(out)
+
+    # host-side bookkeeping of raw fields the engine state does not hold (DouDizhu's trace and suit-level hands)
+    def _after_deal(self):
+        pass
+
+    def _after_step(self, player, decoded):
+        pass
+
+    def _after_step_back(self):
+        pass
 
     def _legal_value(self, action_id):
         return None
@@ -303,7 +333,7 @@ class Env(object):
     def _obs_of(self, obs_bytes, player_id):
         return obs_bytes.astype(np.float64)
 
-    def _raw_obs(self, player_id, legal):
+    def _raw_obs(self, player_id, legal, via):
         return None
 
     def _payoff_array(self, r):

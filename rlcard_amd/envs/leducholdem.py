@@ -34,11 +34,26 @@ class LeducholdemEnv(Env):
         return dict(h=[w0 & 7, (w0 >> 3) & 7], pub=(w0 >> 6) & 7, chips=[(w0 >> 9) & 31, (w0 >> 14) & 31],
                     rc=w1 & 3, ptr=(w1 >> 2) & 1)
 
-    def _raw_obs(self, player_id, legal):
+    def _raw_obs(self, player_id, legal, via):
         f = self._fields()
         return {'hand': CARDS[f['h'][player_id]], 'public_card': CARDS[f['pub']] if f['rc'] >= 1 else None,
                 'all_chips': f['chips'], 'my_chips': f['chips'][player_id],
                 'legal_actions': [self.actions[i] for i in legal], 'current_player': f['ptr']}
+
+    def _payoff_array(self, r):
+        """Game.get_payoffs (leducholdem/game.py:170-178): judger chips / big blind in float64. Heads-up payoffs are
+        multiples of 0.5, exact in the engine's f32 reward row; with 3+ players a split pot pays
+        float(total) / #winners (judger.py:50-56), so the payoffs are rebuilt in float64 with the reference's
+        operations: the winners are the players whose reward is not -in_chips / 2 (each_win > 0)."""
+        r = np.asarray(r, dtype=np.float64)
+        if self.num_players <= 2 or self._payoffs is None or self._words is None:
+            return r
+        chips = self._fields()['chips']
+        won = [float(r[i]) != -chips[i] / 2.0 for i in range(self.num_players)]
+        if not any(won):
+            return r
+        each_win = float(sum(chips)) / sum(won)
+        return np.array([(each_win - c) if w else float(-c) for c, w in zip(chips, won)]) / 2
 
     def get_perfect_information(self):
         f = self._fields()

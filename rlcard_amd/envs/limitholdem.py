@@ -44,14 +44,15 @@ class LimitholdemEnv(Env):
                     board=[(w1 >> (6 * k)) & 63 for k in range(nboard)], chips=[(w0 >> 24) & 63, w2 & 63],
                     ptr=(w0 >> 30) & 1, rc=rc, raise_nums=[(w3 >> (3 * k)) & 7 for k in range(4)])
 
-    def _raw_obs(self, player_id, legal):
+    def _raw_obs(self, player_id, legal, via):
         f = self._fields()
         return {'hand': [card_str(c) for c in f['hands'][player_id]], 'public_cards': [card_str(c) for c in f['board']],
                 'all_chips': f['chips'], 'my_chips': f['chips'][player_id],
                 'legal_actions': [self.actions[i] for i in legal], 'raise_nums': f['raise_nums']}
 
     def get_perfect_information(self):
+        """envs/limitholdem.py:98-109 (no current_round, unlike Leduc; no board -> None)."""
         f = self._fields()
-        return {'chips': f['chips'], 'public_card': [card_str(c) for c in f['board']],
-                'hand_cards': [[card_str(c) for c in h] for h in f['hands']], 'current_round': f['rc'],
+        return {'chips': f['chips'], 'public_card': [card_str(c) for c in f['board']] or None,
+                'hand_cards': [[card_str(c) for c in h] for h in f['hands']],
                 'current_player': f['ptr'], 'legal_actions': [self.actions[i] for i in self._legal_ids(self._last)]}

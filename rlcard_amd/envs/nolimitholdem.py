@@ -67,13 +67,13 @@ class NolimitholdemEnv(Env):
                     board=[(w1 >> (6 * k)) & 63 for k in range(nboard)], chips=chips,
                     stakes=[stack - c for c in chips], ptr=(w0 >> 24) & 1, rc=rc)
 
-    def _raw_obs(self, player_id, legal):
+    def _raw_obs(self, player_id, legal, via):
         """Game.get_state (game.py:187-205): the player's view plus stakes, pot and stage."""
         f = self._fields()
         return {'hand': [card_str(c) for c in f['hands'][player_id]],
                 'public_cards': [card_str(c) for c in f['board']], 'all_chips': f['chips'],
                 'my_chips': f['chips'][player_id], 'legal_actions': [Action(i) for i in legal],
-                'stakes': f['stakes'], 'current_player': f['ptr'], 'pot': sum(f['chips']),
+                'stakes': f['stakes'], 'current_player': f['ptr'], 'pot': np.int64(sum(f['chips'])),   # np.sum
                 'stage': Stage(min(f['rc'], 3))}
 
     def _payoff_array(self, r):

@@ -215,9 +215,22 @@ class VecEnv:
 
     @property
     def rng_first_refill(self):
-        """Draws before an env's first refill: seeding generates the ring's first SLOTS - 1 blocks and a refill runs
-        once the stream is inside the latest (doudizhu: inside its second word block)."""
+        """Draws before the first refill, worst case over the envs (rng_first_refill_of): the lane games' seeding
+        generates 1 + e % (SLOTS - 1) ring blocks for env e (cs_ring.h seed_blocks) and a refill runs once the stream
+        is inside the latest, so env e first refills after (e % (SLOTS - 1)) x 624 draws, at most (SLOTS - 2) x 624;
+        doudizhu twists its next word block 624 draws in."""
         return self.rng_period - 2 * 624 if self.env_id != 'doudizhu' else 624
+
+    def rng_first_refill_of(self, env):
+        """Draws before env `env`'s first refill (global env id: env_base + env)."""
+        if self.env_id == 'doudizhu':
+            return 624
+        return ((self.env_base + int(env)) % (self.rng_period // 624 - 1)) * 624
+
+    @property
+    def rng_per_refill(self):
+        """Draws between two refills: SLOTS - 1 blocks per ring refill; doudizhu one block."""
+        return self.rng_period - 624 if self.env_id != 'doudizhu' else 624
 
     # heads-up hold'em games keep a deal queue after their 4 game words (rlcard_amd/csrc/cs_limit.h): deals drawn
     # ahead. 3..6-player hold'em has none (its judge may draw from the stream at a game's end, cs_holdem_n.h).

@@ -33,6 +33,7 @@ Usage:  python tests/golden/gen_golden.py [--only NAME ...]
 """
 import argparse
 import hashlib
+import json
 import os
 import shutil
 import sys
@@ -58,6 +59,7 @@ def setup_reference():
         typing.Self = typing.Any
     sys.path.insert(0, os.path.join(WORK, 'stubs'))
     sys.path.insert(0, WORK)
+    sys.path.insert(0, os.path.dirname(OUT))   # tests/ (rawcanon)
     sys.dont_write_bytecode = True
 
 
@@ -337,6 +339,25 @@ def gen_blackjack():
     print('blackjack.npz: %d events, run_random(42) trajectory length %d' % (len(st.obs), len(seq_obs)))
 
 
+def gen_blackjack_shoe():
+    """Blackjack beyond one deck / four players (games/blackjack/dealer.py:6-37: deck * num_decks, shuffled, then
+    choice(len(deck)) + pop; game.py:15-54 any game_num_players): shoes of 2..8 decks (8 decks = 416 cards, so the
+    shuffle and the deals draw random_interval with masks past 8 bits) and tables of 1..7 players, plus the infinite
+    deck (0) at 5 players and one deck at 6."""
+    cfgs = [(2, 1), (2, 5), (3, 7), (4, 1), (4, 5), (4, 7), (6, 1), (6, 5), (6, 7), (8, 1), (8, 5), (8, 7), (0, 5),
+            (1, 6), (5, 3)]
+    seeds = [101 + 13 * i for i in range(len(cfgs))]
+    configs = [{'game_num_decks': d, 'game_num_players': p} for d, p in cfgs]
+    st = Stream(2, 2, max(p for _, p in cfgs))
+
+    def pick(rng, state, env):
+        return rng.randrange(2)
+    drive('blackjack', configs, seeds, 25, st, pick)
+    st.save(os.path.join(OUT, 'blackjack_shoe.npz'), seeds, env_decks=np.array([d for d, _ in cfgs], np.int32),
+            env_np=np.array([p for _, p in cfgs], np.int32))
+    print('blackjack_shoe.npz: %d events' % len(st.obs))
+
+
 def gen_doudizhu():
     # 8 seeds x 25 games = 200 games (~12 k events): every seed's stream runs far past its first MT block refills
     seeds = [0, 1, 42, 7, 12941, 2 ** 33 + 1, 99991, 123456789]
@@ -391,6 +412,103 @@ def gen_cfr():
     np.savez_compressed(os.path.join(OUT, 'cfr.npz'), seeds=np.array([s for s, _ in runs], np.int64),
                         iterations=np.array([k for _, k in runs], np.int64), **out)
     print('cfr.npz: %s' % ', '.join('seed %d x %d it' % x for x in runs))
+
+
+# --------------------------------------------------------------------------------------------------------------
+# The rlcard API's raw side: raw_obs, raw_legal_actions, legal_actions key order, action_record,
+# get_perfect_information, get_payoffs (tests/rawcanon.py encodes them as canonical JSON)
+# --------------------------------------------------------------------------------------------------------------
+class RawStream:
+    """Per event: stream index, kind (0 reset, 1 step, 2 step_back, 3 Env.get_state(p) after the game), the action id
+    fed (kind 1) or the player asked for (kind 3), the returned player, is_over, and three JSON strings: the state
+    view, get_perfect_information() (or the exception it raised) and get_payoffs() (at the step that ends a game;
+    called once per game, as Env.run does -- with 3+ hold'em players it may draw from the env's stream)."""
+
+    def __init__(self):
+        self.cols = {k: [] for k in ('stream', 'kind', 'act', 'player', 'done')}
+        self.state, self.perfect, self.payoffs = [], [], []
+
+    def add(self, si, kind, act, state, player, env, payoffs=None):
+        import rawcanon
+        if env.name == 'doudizhu':
+            from rlcard.games.doudizhu.utils import ACTION_2_ID
+            state = rawcanon.ddz_sort_leading(state, ACTION_2_ID)
+        for k, v in zip(self.cols, (si, kind, act, player, int(env.is_over()))):
+            self.cols[k].append(int(v))
+        self.state.append(rawcanon.dumps(rawcanon.state_view(state)))
+        try:
+            info = env.get_perfect_information()
+            if env.name == 'doudizhu':
+                info = rawcanon.ddz_sort_perfect(info, ACTION_2_ID)
+            self.perfect.append(rawcanon.dumps(info))
+        except NotImplementedError:
+            self.perfect.append('"NotImplementedError"')
+        self.payoffs.append('' if payoffs is None else rawcanon.dumps(payoffs))
+
+    def save(self, path, streams):
+        d = {k: np.array(v, dtype=np.int32) for k, v in self.cols.items()}
+        d.update(state=np.array(self.state), perfect=np.array(self.perfect), payoffs=np.array(self.payoffs),
+                 streams=np.array([json.dumps(s, sort_keys=True) for s in streams]))
+        np.savez_compressed(path, **d)
+
+
+def drive_raw(rec, si, env_id, cfg, seed, games, sb_prob, pick):
+    import random
+    import rlcard
+    env = rlcard.make(env_id, config=dict(cfg, seed=seed, allow_step_back=sb_prob > 0))
+    rng = random.Random(7777 * (si + 1) + seed)
+    for _ in range(games):
+        state, player = env.reset()
+        rec.add(si, 0, -1, state, player, env)
+        nsteps = 0
+        while not env.is_over():
+            if sb_prob > 0 and rng.random() < sb_prob:
+                r = env.step_back()
+                if r is not False:
+                    state, player = r
+                    rec.add(si, 2, -1, state, player, env)
+                    continue
+            a = pick(rng, state, env)
+            state, player = env.step(a)
+            rec.add(si, 1, a, state, player, env, env.get_payoffs() if env.is_over() else None)
+            nsteps += 1
+            assert nsteps < 10000
+        for p in range(env.num_players):
+            rec.add(si, 3, p, env.get_state(p), p, env)
+
+
+def pick_legal(rng, state, env):
+    return rng.choice(sorted(state['legal_actions'].keys()))
+
+
+def gen_raw():
+    """raw_<game>.npz: streams (env id config, seed, games, step_back probability) replayed by tests/test_raw.py
+    through rlcard_amd.make with the same action ids and step_back calls."""
+    specs = {
+        'leduc': [('leduc-holdem', {}, 0, 25, 0.0, pick_holdem), ('leduc-holdem', {}, 42, 25, 0.0, pick_holdem),
+                  ('leduc-holdem', {}, 3, 12, 0.3, pick_holdem)],
+        'limit': [('limit-holdem', {}, 0, 20, 0.0, pick_holdem), ('limit-holdem', {}, 5, 20, 0.0, pick_holdem),
+                  ('limit-holdem', {}, 7, 8, 0.3, pick_holdem),
+                  ('limit-holdem', {'game_num_players': 4}, 11, 10, 0.0, pick_holdem)],
+        'nolimit': [('no-limit-holdem', {}, 0, 20, 0.0, pick_legal),
+                    ('no-limit-holdem', {'chips_for_each': 12, 'dealer_id': 1}, 42, 20, 0.0, pick_legal),
+                    ('no-limit-holdem', {}, 9, 8, 0.3, pick_legal),
+                    ('no-limit-holdem', {'game_num_players': 3, 'chips_for_each': 10}, 13, 12, 0.0, pick_legal),
+                    ('no-limit-holdem', {'game_num_players': 6}, 17, 6, 0.0, pick_legal)],
+        'blackjack': [('blackjack', {}, 0, 25, 0.0, lambda rng, s, e: rng.randrange(2)),
+                      ('blackjack', {}, 42, 25, 0.0, lambda rng, s, e: rng.randrange(2)),
+                      ('blackjack', {'game_num_players': 3}, 5, 15, 0.0, lambda rng, s, e: rng.randrange(2))],
+        'doudizhu': [('doudizhu', {}, 0, 2, 0.0, pick_legal), ('doudizhu', {}, 42, 1, 0.0, pick_legal),
+                     ('doudizhu', {}, 1, 2, 0.25, pick_legal), ('doudizhu', {}, 12941, 2, 0.0, pick_legal)],
+    }
+    for name, streams in specs.items():
+        rec = RawStream()
+        meta = []
+        for si, (env_id, cfg, seed, games, sb, pick) in enumerate(streams):
+            drive_raw(rec, si, env_id, cfg, seed, games, sb, pick)
+            meta.append({'env_id': env_id, 'config': cfg, 'seed': seed, 'games': games, 'step_back': sb > 0})
+        rec.save(os.path.join(OUT, 'raw_%s.npz' % name), meta)
+        print('raw_%s.npz: %d events (%d step_back)' % (name, len(rec.state), rec.cols['kind'].count(2)))
 
 
 # --------------------------------------------------------------------------------------------------------------
@@ -528,7 +646,7 @@ RANK_CHARS = '3456789TJQKA2BR'
 def gen_ddz_table():
     """The DouDizhu action-id space (games/doudizhu/jsondata: action_space.txt, card_type.json) as numbers:
     id -> rank counts (3..A,2,B,R), type index, weight. This is the action contract itself (27 472 ids)."""
-    from rlcard.games.doudizhu.utils import ID_2_ACTION, CARD_TYPE, TYPE_CARD
+    from rlcard.games.doudizhu.utils import ID_2_ACTION, ACTION_2_ID, CARD_TYPE, TYPE_CARD
     type_names = list(TYPE_CARD.keys())
     n = len(ID_2_ACTION)
     counts = np.zeros((n, 15), dtype=np.uint8)
@@ -542,8 +660,17 @@ def gen_ddz_table():
         (t, w), = CARD_TYPE[0][a]
         ttype[i] = type_names.index(t)
         weight[i] = int(w)
+    # position of each id in its type's TYPE_CARD enumeration (weights, then the card lists): the order get_gt_cards
+    # (utils.py:225-262) lists a following player's legal actions in; not the id order for trio_solo_chain_2..5
+    tc_order = np.zeros(n, dtype=np.int32)
+    for t, by_weight in TYPE_CARD.items():
+        k = 0
+        for _, cards_list in by_weight.items():
+            for cards in cards_list:
+                tc_order[ACTION_2_ID[cards]] = k
+                k += 1
     digest = hashlib.sha256(' '.join(ID_2_ACTION).encode()).hexdigest()
-    np.savez_compressed(os.path.join(OUT, 'ddz_actions.npz'), counts=counts, type=ttype, weight=weight,
+    np.savez_compressed(os.path.join(OUT, 'ddz_actions.npz'), counts=counts, type=ttype, weight=weight, tc_order=tc_order,
                         type_names=np.array(type_names), pass_id=np.int32(ID_2_ACTION.index('pass')),
                         action_space_sha256=np.array(digest))
     print('ddz_actions.npz: %d ids, %d types, sha256 %s' % (n, len(type_names), digest[:16]))
@@ -610,7 +737,7 @@ def main():
     gens = {'mt19937': gen_mt, 'leduc': gen_leduc, 'limit': gen_limit, 'blackjack': gen_blackjack,
             'doudizhu': gen_doudizhu, 'nolimit': gen_nolimit, 'cfr': gen_cfr, 'holdem_eval': gen_holdem_eval,
             'holdem_ref_kats': gen_holdem_ref_kats, 'ddz_table': gen_ddz_table,
-            'ddz_judger': gen_ddz_judger, 'nplayer': gen_nplayer}
+            'ddz_judger': gen_ddz_judger, 'nplayer': gen_nplayer, 'raw': gen_raw, 'blackjack_shoe': gen_blackjack_shoe}
     for name, fn in gens.items():
         if args.only is None or name in args.only:
             fn()

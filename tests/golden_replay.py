@@ -25,6 +25,8 @@ def env_config(d, ei):
     c = {}
     if 'env_np' in d.files:
         c['game_num_players'] = int(d['env_np'][ei])
+    if 'env_decks' in d.files:
+        c['game_num_decks'] = int(d['env_decks'][ei])
     if 'env_chips' in d.files:
         dealer = int(d['env_dealer'][ei])
         c.update({'chips_for_each': int(d['env_chips'][ei]), 'dealer_id': None if dealer < 0 else dealer})

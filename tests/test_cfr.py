@@ -61,8 +61,9 @@ def test_cfr_agent_matches_reference_agent():
 
 @pytest.mark.gpu
 def test_cfr_batched_deals_match_oracle(oracle):
-    """B envs = B deals per player per iteration: tables vs the oracle's (players outer, envs inner); fp64 atomics
-    reorder the sums, so values match to 1e-9 relative; keys, and every env's RNG position, match exactly."""
+    """B envs = B deals per player per iteration: tables vs the oracle's (players outer, envs inner), bit-exact: the
+    deals' contributions are reduced in the oracle's order (cs_cfr.hip records + stable sort), not by atomics; keys
+    and every env's RNG position match exactly."""
     _need_gpu()
     from rlcard_amd import VecEnv
     from rlcard_amd.agents import CFRAgent
@@ -80,8 +81,7 @@ def test_cfr_batched_deals_match_oracle(oracle):
     for name, bit in (('policy', 1), ('average_policy', 2), ('regrets', 2)):
         rows = (t['flags'] & bit) != 0          # keys of the dict (unkeyed rows hold the tables' initial values)
         assert rows.sum() > 50
-        np.testing.assert_allclose(host[name][rows], t[name][rows], rtol=1e-9, atol=1e-9 * np.abs(t[name]).max(),
-                                   err_msg=name)
+        assert np.array_equal(host[name][rows], t[name][rows]), name
     for i in (0, 1, B // 2, B - 1):
         assert v.rng_position(i) == c.draws(i) % v.rng_period
 

@@ -142,3 +142,21 @@ def test_dmc_actor_fills_learner_batches():
             total[p] += ids.numel()
     assert not actor.buffers.dropped()
     assert sum(total.values()) > 0
+
+
+def test_actor_buffers_overflow_raises_and_lists_no_stale_chunk():
+    """A ring too small for one fill (slots = 2, chunks never gathered): rows that would overwrite a chunk not yet
+    handed out are dropped, not counted (no listed chunk holds one) and fill() raises."""
+    from rlcard_amd import VecEnv, _abi
+    from rlcard_amd.agents.dmc_agent import ActorBuffers
+    v = VecEnv('leduc-holdem', 64, seed=5)
+    v.reset()
+    buf = ActorBuffers(v, T=4, slots=2)
+    tr = v.rollout(6, policy_seed=1)
+    ready = buf.fill(tr)                     # <= 6 rows per (env, player): fits the two 4-row chunks
+    assert not buf.dropped()
+    assert int(ready.numel()) <= 64 * 2 * 2
+    with pytest.raises(_abi.CardsimError, match='overflowed'):
+        for k in range(4):
+            buf.fill(v.rollout(64, policy_seed=1, t0=6 + 64 * k))
+    assert buf.dropped()

@@ -129,3 +129,33 @@ def test_nplayer_compat_env(game, players):
         for p in range(players):
             raw = traj[p][-1]['raw_obs']
             assert len(raw['all_chips']) == players
+
+
+def test_leduc_nplayer_payoffs_exact_float64():
+    """N-player Leduc through rlcard_amd.make: Env.get_payoffs equals the reference's float64 payoffs exactly
+    (float(total) / #winners, leducholdem/judger.py:50-56, / big blind), unrounded, for every game of leduc_np.npz
+    (3..5 players, three-way splits included). The engine's reward rows are f32 (ABI); the compat Env rebuilds the
+    float64 values with the reference's operations."""
+    import rlcard_amd
+    d = gr.load('leduc_np')
+    checked = nonbinary = 0
+    env, cur = None, -1
+    for k in range(len(d['ev_env'])):
+        ei = int(d['ev_env'][k])
+        if ei != cur:
+            env = rlcard_amd.make('leduc-holdem', config={'seed': int(d['seeds'][ei]),
+                                                          'game_num_players': int(d['env_np'][ei])})
+            cur = ei
+        if d['ev_kind'][k] == 0:
+            env.reset()
+            continue
+        env.step(int(d['ev_act'][k]))
+        assert int(env.is_over()) == int(d['ev_done'][k])
+        if d['ev_done'][k]:
+            n = env.num_players
+            got, exp = env.get_payoffs(), d['ev_payoff'][k][:n]
+            assert got.dtype == np.float64 and np.array_equal(got, exp), (k, got, exp)
+            checked += 1
+            nonbinary += int(np.any(exp * 2 != np.round(exp * 2)))   # split pots with an odd total
+    # a Leduc deck holds two cards per rank, so at most two players split: the values are multiples of 0.25
+    assert checked > 100, (checked, nonbinary)

@@ -1,8 +1,8 @@
 """Parity past the MT19937 refills, at the shapes bench.py times.
 
-A freshly seeded lane-game env (Leduc, Limit, No-limit, Blackjack) holds ring blocks 0..SLOTS-2 and first refills once
-its stream is inside block L (position >= rng_period - 2 x 624: 3 744 draws with 8 slots, cs_ring.h `needs_refill`),
-then every (SLOTS - 1) x 624 draws; DouDizhu's two-block word
+A freshly seeded lane-game env e (Leduc, Limit, No-limit, Blackjack) holds ring blocks 0..e % (SLOTS - 1) and first
+refills once its stream is inside the latest (after (e % 15) x 624 draws with the 16-slot ring, cs_ring.h seed_blocks /
+`needs_refill`), then every (SLOTS - 1) x 624 = 9 360 draws; DouDizhu's two-block word
 window first twists at ~1 184 draws (cs_doudizhu.hip `WaveMt::window`). The tests below drive every env well past
 two refills and compare every launch with the CPU oracle, so the paths the timed launches run in steady state
 (ring_refill_wave's multi-block twist, ring_gen_serial, the batched restage after a refill, Leduc's reset_swar across block
@@ -75,56 +75,67 @@ def test_doudizhu_past_mt_twists(oracle):
     _roll_past_refills(oracle, 'doudizhu', 64, 64, 22, 0, 42, 1300)
 
 
-def test_leduc_full_size_after_precondition(oracle):
-    """The bench's 2^20 Leduc envs after 14 preconditioning launches (T = 256): one timed-shape launch is then
-    compared with the oracle on three windows (start, middle, end) replayed from seeding with the same env ids."""
-    n, T, win, pre = 1 << 20, 256, 256, 14
-    v = _vec('leduc-holdem', n, seed=42)
+@pytest.mark.parametrize('game,win', [('leduc-holdem', 256), ('limit-holdem', 256), ('no-limit-holdem', 256),
+                                      ('blackjack', 256), ('doudizhu', 48)])
+def test_full_size_after_precondition(oracle, game, win):
+    """Every bench.py shape exactly as bench.py runs it: the BASELINE env count and fused steps per launch
+    (bench.GAMES: Leduc 2^20 x 256, Limit / No-limit 262 144 x 256, Blackjack 2^20 x 64, DouDizhu 65 536 x 64), the
+    same seeds and policy, bench.precondition_launches untimed launches, then one timed-shape launch compared with the
+    oracle on three windows (start, middle, end) replayed from seeding with the same global env ids. Every env of a
+    window has passed its first refill (hold'em deal queues, Blackjack's shoe draws and DouDizhu's word window
+    included)."""
+    import bench
+    g = bench.GAMES[game]
+    n, T = g['envs'], g['T']
+    v = _vec(game, n, seed=42)
     v.reset()
     out = v.new_traj_out(T)
+    pre = bench.precondition_launches(game, T, v)
     for c in range(pre):
         v.rollout(T, policy_seed=5, t0=c * T, out=out)
     tr = v.rollout(T, policy_seed=5, t0=pre * T, out=out)
     torch.cuda.synchronize()
     for start in (0, n // 2 + 17, n - win):
-        ob = _oracle_batch(oracle, 'leduc-holdem', range(42 + start, 42 + start + win))
+        ob = _oracle_batch(oracle, game, range(42 + start, 42 + start + win))
         ob.reset()
         for c in range(pre):
             ob.rollout(T, 5, c * T, start)
         exp = ob.rollout(T, 5, pre * T, start)
         got = {k: x[:, start:start + win].cpu().numpy() for k, x in tr.items()}
-        _assert_same(got, exp, 'window %d' % start)
+        _assert_same(got, exp, '%s window %d' % (game, start))
         d = _draws(ob, win)
-        assert d.min() >= v.rng_first_refill + 300, 'window %d has not refilled (min draws %d)' % (start, d.min())
+        first = np.array([v.rng_first_refill_of(start + i) for i in range(win)])
+        assert (d >= first + 300).all(), 'window %d: an env has not refilled (%d)' % (start, (d - first).min())
         for i in (0, win - 1):
             assert v.rng_position(start + i) == d[i] % v.rng_period
 
 
 def test_cfr_batched_past_refills(oracle):
-    """Batched chance-sampling CFR for enough iterations that every env's stream refills (each iteration deals once
-    per player): tables to 1e-9, RNG positions exactly."""
+    """Batched chance-sampling CFR for 1 000 iterations (each deals once per player, ~14.6 draws): every env's
+    stream passes its staggered first refill ((e % 15) x 624 draws, cs_ring.h seed_blocks) by >= 300 draws. Tables
+    bit-exact with the oracle (ordered reduction, cs_cfr.hip), and a second run gives the same bits."""
     from rlcard_amd import VecEnv
     from rlcard_amd.agents import CFRAgent
-    B, K = 256 + 3, 400
-    v = VecEnv('leduc-holdem', B, seed=21)
-    agent = CFRAgent(v)
-    agent.train(K)
-    torch.cuda.synchronize()
+    B, K = 256 + 3, 1000
+    tabs = []
+    for run in range(2):
+        v = VecEnv('leduc-holdem', B, seed=21)
+        agent = CFRAgent(v)
+        agent.train(K)
+        torch.cuda.synchronize()
+        tabs.append(agent._tables())
     keys, lens = seeding.seed_keys(range(21, 21 + B))
     c = oracle.CFR(keys, lens)
     c.train(K)
     d = np.array([c.draws(i) for i in range(B)])
-    # env e's first refill comes after (e % 15) x 624 draws (cs_ring.h seed_blocks): most streams are past it
-    first = (np.arange(B) % 15) * 624
-    assert (d >= first + 300).mean() > 0.5, (d - first).min()
+    first = np.array([v.rng_first_refill_of(e) for e in range(B)])
+    assert (d >= first + 300).all(), (d - first).min()
     t = c.tables()
-    host = agent._tables()
+    host = tabs[0]
     assert np.array_equal(host['flags'].astype(np.uint8), t['flags'])
     for name, bit in (('policy', 1), ('average_policy', 2), ('regrets', 2)):
         rows = (t['flags'] & bit) != 0
-        # fp64 atomics add the 259 deals of an iteration in any order, so the rounding differences grow with the
-        # iterations: 1e-9 holds at K = 400 (at 700-800, 1e-8 absolute on a policy entry near zero was seen)
-        np.testing.assert_allclose(host[name][rows], t[name][rows], rtol=1e-9, atol=1e-9 * np.abs(t[name]).max(),
-                                   err_msg=name)
+        assert np.array_equal(host[name][rows], t[name][rows]), name
+        assert np.array_equal(tabs[0][name], tabs[1][name]), name + ' differs between two identical runs'
     for i in (0, 1, 63, 64, B // 2, B - 1):
         assert v.rng_position(i) == d[i] % v.rng_period

@@ -1,0 +1,82 @@
+#!/bin/bash
+# The one GPU-box driver (replaces round 1-2's one-off tools/gpu_*.sh A/B scripts). Libraries are prebuilt in-tree
+# on the CPU container; nothing is compiled here.
+#
+#   TAG=name bash tools/gpu.sh STEP [STEP ...]
+#
+# Steps run in order, each under its own time limit; the first failing step ends the call (no retries).
+#   tests[:K_EXPR]            pytest -m gpu [-k K_EXPR]                         -> tests.log
+#   smoke                     __graft_entry__.smoke()                           -> smoke.log
+#   bench:GAME[:ARGS...]      python bench.py --game GAME ARGS (ARGS ','-separated) -> bench_GAME.jsonl
+#   counters:GAME:N:T         SQ instruction / wait counters over tools/ab_rollout.py, one PMC pass per group
+#   profile:GAME[:ARGS...]    kernel trace + stats, then FETCH_SIZE and WRITE_SIZE passes over bench.py
+#   ab:GAME:N:T:F1[:F2...]    tools/ab_rollout.py kernel-flag A/B (AB_PLAYERS / AB_WARM from the env)
+#   abl:GAME:N:T:LIB1[:LIB2]  the same rollout timed with several library builds (CARDSIM_LIB), interleaved runs
+set -o pipefail
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" || exit 2
+O=$R/gpurun_out/${TAG:-run}
+mkdir -p "$O"
+echo "host $(hostname) $(date -u +%FT%TZ) head $(cat .git_head 2>/dev/null)" >> "$O/steps.log"
+
+run() {   # run LIMIT LOG cmd...
+  local lim=$1 log=$2; shift 2
+  echo "[$(date -u +%T)] $*" >> "$O/steps.log"
+  timeout -k 10 "$lim" "$@" > "$log" 2>&1
+  local rc=$?
+  echo "[$(date -u +%T)] rc=$rc" >> "$O/steps.log"
+  if [ $rc -ne 0 ]; then tail -30 "$log"; exit $rc; fi
+}
+
+for step in "$@"; do
+  IFS=':' read -r -a a <<< "$step"
+  case "${a[0]}" in
+    tests)
+      if [ -n "${a[1]}" ]; then
+        run 900 "$O/tests.log" python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${a[1]}"
+      else
+        run 1000 "$O/tests.log" python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+      fi
+      tail -3 "$O/tests.log" ;;
+    smoke)
+      run 300 "$O/smoke.log" python3 -c "import __graft_entry__ as g; g.smoke()"
+      tail -6 "$O/smoke.log" ;;
+    bench)
+      g=${a[1]}; extra=$(echo "${a[*]:2}" | tr ',' ' ')
+      run 400 "$O/bench_$g.err" python3 bench.py --game "$g" $extra
+      grep '^{' "$O/bench_$g.err" > "$O/bench_$g.jsonl"; cat "$O/bench_$g.jsonl" ;;
+    counters)
+      g=${a[1]}; n=${a[2]}; t=${a[3]}; d=$O/cnt_$g; mkdir -p "$d"; i=0
+      for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
+                 "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_BRANCH" \
+                 "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM" \
+                 "FETCH_SIZE" "WRITE_SIZE" \
+                 "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM"; do
+        i=$((i+1))
+        run 240 "$d/run$i.log" rocprofv3 --pmc $grp --output-format csv -d "$d/p$i" -o p -- python3 tools/ab_rollout.py "$g" "$n" "$t" 0
+      done
+      python3 tools/pmc_summary.py "$d" > "$d/summary.txt" 2>&1; cat "$d/summary.txt" ;;
+    profile)
+      g=${a[1]}; extra=$(echo "${a[*]:2}" | tr ',' ' '); d=$O/prof_$g; mkdir -p "$d"
+      B="bench.py --game $g --no-cpu-baseline --no-philox --gather none --steps ${STEPS:-100} $extra"
+      run 300 "$d/bench_kt.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$d/kt" -o kt -- python3 $B
+      run 300 "$d/bench_fetch.log" rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$d/fetch" -o fetch -- python3 $B
+      run 300 "$d/bench_write.log" rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$d/write" -o write -- python3 $B
+      grep '^{' "$d/bench_kt.log" | tail -1 ;;
+    ab)
+      run 400 "$O/ab_${a[1]}.log" python3 tools/ab_rollout.py "${a[1]}" "${a[2]}" "${a[3]}" "${a[@]:4}"
+      cat "$O/ab_${a[1]}.log" ;;
+    abl)
+      g=${a[1]}; n=${a[2]}; t=${a[3]}
+      for rnd in 1 2 3; do
+        for lib in "${a[@]:4}"; do
+          echo "== $lib round $rnd" >> "$O/abl_$g.log"
+          CARDSIM_LIB=$lib run 300 "$O/abl_tmp.log" python3 tools/ab_rollout.py "$g" "$n" "$t" 0
+          sed "s|^|$lib |" "$O/abl_tmp.log" >> "$O/abl_$g.log"
+        done
+      done
+      cat "$O/abl_$g.log" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
