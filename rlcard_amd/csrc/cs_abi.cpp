@@ -97,7 +97,10 @@ int cs_create(cs_handle** out, int32_t game, int64_t num_envs, int32_t device, c
     if ((r = set_device(h)) != CS_OK) { delete h; return r; }
     const size_t n = (size_t)num_envs;
     // u32 per env of the MT stream: doudizhu's two word blocks, the others' byte ring (info.rng_period bytes + wbuf)
-    const size_t mtw = info.rng_period == 2 * 624 ? (size_t)(2 * 624) : (size_t)cs::RING_ENV_WORDS_HOST;
+    // (Blackjack shoes: one 624-word column per env, cs_blackjack_shoe.hip)
+    const size_t mtw = info.rng_period == 2 * 624 ? (size_t)(2 * 624)
+                       : info.rng_period == 624   ? (size_t)624
+                                                  : (size_t)cs::RING_ENV_WORDS_HOST;
     if ((e = hipMalloc((void**)&h->b.mt, n * mtw * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc((void**)&h->b.ctl, n * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc((void**)&h->b.state, n * (size_t)info.state_words * sizeof(uint32_t))) != hipSuccess) {
@@ -112,7 +115,7 @@ int cs_create(cs_handle** out, int32_t game, int64_t num_envs, int32_t device, c
         }
         h->b.table = &h->tab;
     }
-    const int64_t sb = cs::stage_bytes_per_env(game, info.num_players);
+    const int64_t sb = cs::stage_bytes_per_env(game, info.num_players, h->b.num_decks);
     if (sb > 0) {   // rollout staging rows, whole waves (the copy moves 16-B chunks of full rows)
         const size_t rows = (n + 63) / 64 * 64;
         if ((e = hipMalloc((void**)&h->b.sctl, n * sizeof(uint32_t))) != hipSuccess ||

@@ -57,7 +57,7 @@ struct DmcRing {
 };
 
 int game_info(int32_t game, const cs_config* cfg, cs_game_info* info);
-int64_t stage_bytes_per_env(int32_t game, int32_t num_players);
+int64_t stage_bytes_per_env(int32_t game, int32_t num_players, int32_t num_decks);
 inline bool state_env_major(int32_t game) { return game == CS_GAME_DOUDIZHU; }
 
 hipError_t launch_seed(const Buffers& b, const uint32_t* keys_dev, const int32_t* klen_dev, int64_t first,
@@ -89,6 +89,17 @@ hipError_t np10_launch_step(const Buffers& b, const int32_t* actions, const cs_s
 hipError_t np10_launch_observe(const Buffers& b, int32_t player, const cs_step_out& o, hipStream_t s);
 hipError_t np10_launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
                                const cs_traj_out& o, hipStream_t s);
+// cs_blackjack_shoe.hip: Blackjack with 2..8-deck shoes or 5..7 players (word-stream RNG, materialised shoe)
+bool is_blackjack_shoe(const Buffers& b);
+int bjs_game_info(const cs_config* cfg, cs_game_info* info);
+hipError_t bjs_launch_seed(const Buffers& b, const uint32_t* keys_dev, const int32_t* klen_dev, int64_t first,
+                           int64_t count, hipStream_t s);
+hipError_t bjs_launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s);
+hipError_t bjs_launch_step(const Buffers& b, const int32_t* actions, const cs_step_out& o, hipStream_t s);
+hipError_t bjs_launch_observe(const Buffers& b, int32_t player, const cs_step_out& o, hipStream_t s);
+hipError_t bjs_launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
+                              const cs_traj_out& o, hipStream_t s);
+
 inline bool is_holdem_n(const Buffers& b)
 {
     return (b.game == CS_GAME_LEDUC || b.game == CS_GAME_LIMIT || b.game == CS_GAME_NOLIMIT) && b.num_players > 2;

@@ -11,8 +11,9 @@
 
 namespace cs {
 
-int64_t stage_bytes_per_env(int32_t game, int32_t num_players)
+int64_t stage_bytes_per_env(int32_t game, int32_t num_players, int32_t num_decks)
 {
+    if (game == CS_GAME_BLACKJACK && (num_decks >= 2 || num_players > 4)) return 0;   // cs_blackjack_shoe.hip
     switch (game) {
     case CS_GAME_LEDUC: return num_players > 2 ? np_stage_bytes(game, num_players) : stage_bytes_of<Leduc>();
     case CS_GAME_LIMIT: return num_players > 2 ? np_stage_bytes(game, num_players) : stage_bytes_of<Limit>();
@@ -38,7 +39,7 @@ int game_info(int32_t game, const cs_config* cfg, cs_game_info* info)
     case CS_GAME_BLACKJACK: {
         const int np = (cfg && cfg->num_players > 0) ? cfg->num_players : 1;
         const int nd = (cfg && cfg->num_decks >= 0) ? cfg->num_decks : 1;
-        if (np > 4 || nd > 1) return CS_E_UNSUPPORTED;
+        if (np > 4 || nd > 1) return bjs_game_info(cfg, info);   // shoes and big tables: cs_blackjack_shoe.hip
         if (np == 1) fill_info<Blackjack<1>>(info);
         else if (np == 2) fill_info<Blackjack<2>>(info);
         else if (np == 3) fill_info<Blackjack<3>>(info);
@@ -109,6 +110,7 @@ hipError_t launch_seed(const Buffers& b, const uint32_t* keys, const int32_t* kl
 {
 #define C_(G) seed_g<G>(b, keys, klen, first, count, s)
     if (b.game == CS_GAME_DOUDIZHU) return C_(ddz::SeedView);
+    if (is_blackjack_shoe(b)) return bjs_launch_seed(b, keys, klen, first, count, s);
     if (is_holdem_n(b)) return np_launch_seed(b, keys, klen, first, count, s);
     CS_DISPATCH(b.game, C_)
 #undef C_
@@ -117,6 +119,7 @@ hipError_t launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s)
 {
 #define C_(G) reset_g<G>(b, o, s)
     if (b.game == CS_GAME_DOUDIZHU) return ddz::launch_reset(b, o, s);
+    if (is_blackjack_shoe(b)) return bjs_launch_reset(b, o, s);
     if (is_holdem_n(b)) return np_launch_reset(b, o, s);
     CS_DISPATCH(b.game, C_)
 #undef C_
@@ -125,6 +128,7 @@ hipError_t launch_step(const Buffers& b, const int32_t* a, const cs_step_out& o,
 {
 #define C_(G) step_g<G>(b, a, o, s)
     if (b.game == CS_GAME_DOUDIZHU) return ddz::launch_step(b, a, o, s);
+    if (is_blackjack_shoe(b)) return bjs_launch_step(b, a, o, s);
     if (is_holdem_n(b)) return np_launch_step(b, a, o, s);
     CS_DISPATCH(b.game, C_)
 #undef C_
@@ -133,6 +137,7 @@ hipError_t launch_observe(const Buffers& b, int32_t p, const cs_step_out& o, hip
 {
 #define C_(G) observe_g<G>(b, p, o, s)
     if (b.game == CS_GAME_DOUDIZHU) return ddz::launch_observe(b, p, o, s);
+    if (is_blackjack_shoe(b)) return bjs_launch_observe(b, p, o, s);
     if (is_holdem_n(b)) return np_launch_observe(b, p, o, s);
     CS_DISPATCH(b.game, C_)
 #undef C_
@@ -142,6 +147,7 @@ hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t
 {
 #define C_(G) rollout_g<G>(b, T, seed, t0, env_base, o, s)
     if (b.game == CS_GAME_DOUDIZHU) return ddz::launch_rollout(b, T, seed, t0, env_base, o, s);
+    if (is_blackjack_shoe(b)) return bjs_launch_rollout(b, T, seed, t0, env_base, o, s);
     if (is_holdem_n(b)) return np_launch_rollout(b, T, seed, t0, env_base, o, s);
     CS_DISPATCH(b.game, C_)
 #undef C_

@@ -20,9 +20,18 @@ class BlackjackEnv(Env):
         return obs_bytes.astype(np.int64)          # (player score, dealer's visible score)
 
     def _hands(self):
+        """The hands (players 0..P-1, then the dealer) from the packed state: cs_blackjack.h (1 deck, <= 4 players:
+        sizes 4 bits each in word 30, 12-byte hands from word 15) or cs_blackjack_shoe.hip (168 words: sizes 5 bits
+        each in words 1..2, 24-byte hands from word 120)."""
         w = self._state_words()
-        sizes = w[30]
         hands = []
+        if len(w) == 168:
+            b = np.array(w[120:168], dtype='<u4').view(np.uint8)
+            for h in range(self.num_players + 1):
+                n = (w[1] >> (5 * h)) & 31 if h < 6 else (w[2] >> (5 * (h - 6))) & 31
+                hands.append([card_str(int(c)) for c in b[24 * h:24 * h + n]])
+            return hands
+        sizes = w[30]
         for h in range(self.num_players + 1):
             n = (sizes >> (4 * h)) & 15
             hands.append([card_str((w[15 + (12 * h + k) // 4] >> (8 * ((12 * h + k) % 4))) & 255) for k in range(n)])

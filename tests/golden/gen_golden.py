@@ -497,7 +497,9 @@ def gen_raw():
                     ('no-limit-holdem', {'game_num_players': 6}, 17, 6, 0.0, pick_legal)],
         'blackjack': [('blackjack', {}, 0, 25, 0.0, lambda rng, s, e: rng.randrange(2)),
                       ('blackjack', {}, 42, 25, 0.0, lambda rng, s, e: rng.randrange(2)),
-                      ('blackjack', {'game_num_players': 3}, 5, 15, 0.0, lambda rng, s, e: rng.randrange(2))],
+                      ('blackjack', {'game_num_players': 3}, 5, 15, 0.0, lambda rng, s, e: rng.randrange(2)),
+                      ('blackjack', {'game_num_players': 5, 'game_num_decks': 6}, 9, 8, 0.0,
+                       lambda rng, s, e: rng.randrange(2))],
         'doudizhu': [('doudizhu', {}, 0, 2, 0.0, pick_legal), ('doudizhu', {}, 42, 1, 0.0, pick_legal),
                      ('doudizhu', {}, 1, 2, 0.25, pick_legal), ('doudizhu', {}, 12941, 2, 0.0, pick_legal)],
     }

@@ -157,6 +157,21 @@ static void abi_host()
     for (int g = 0; g < 5; g++) EXPECT(cs_game_info_get(g, &cfg, &info) == CS_OK && info.obs_dim > 0);
     EXPECT(cs_game_info_get(7, &cfg, &info) != CS_OK);
     EXPECT(cs_game_info_get(CS_GAME_LEDUC, &cfg, nullptr) == CS_E_INVALID);
+    // Blackjack shoes / big tables (cs_blackjack_shoe.hip): 8 decks x 7 players; 9 decks, 8 players and the
+    // Philox byte stream are refused
+    cfg.num_players = 7;
+    cfg.num_decks = 8;
+    EXPECT(cs_game_info_get(CS_GAME_BLACKJACK, &cfg, &info) == CS_OK && info.state_words == 168 && info.num_players == 7);
+    cfg.num_decks = 9;
+    EXPECT(cs_game_info_get(CS_GAME_BLACKJACK, &cfg, &info) == CS_E_UNSUPPORTED);
+    cfg.num_decks = 2;
+    cfg.num_players = 8;
+    EXPECT(cs_game_info_get(CS_GAME_BLACKJACK, &cfg, &info) == CS_E_UNSUPPORTED);
+    cfg.num_players = 1;
+    cfg.rng_mode = CS_RNG_PHILOX;
+    EXPECT(cs_game_info_get(CS_GAME_BLACKJACK, &cfg, &info) == CS_E_UNSUPPORTED);
+    cfg.rng_mode = CS_RNG_MT19937;
+    cfg.num_decks = -1;
     cfg.num_players = 9;
     EXPECT(cs_game_info_get(CS_GAME_LEDUC, &cfg, &info) != CS_OK);
     EXPECT(strlen(cs_last_error()) > 0);
