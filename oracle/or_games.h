@@ -32,7 +32,7 @@ static inline void or_shuffle_int(or_mt *rng, int *x, int n)
 
 /* limitholdem/judger.py:11-108 for np players (or_judger.c): value[i] = or_holdem_rank7 of player i's seven cards, 0 =
  * hand None (folded); in_chips = chips bet; payoffs = chips won (may draw np_random.choice for odd split remainders) */
-#define OR_HOLDEM_MAXP 10
+#define OR_HOLDEM_MAXP 23   /* 2P + 5 <= 52 dealt cards */
 void or_holdem_judge(int np, const uint32_t *value, const int *in_chips, or_mt *rng, int *payoffs);
 
 static inline void or_set_bit(uint8_t *bits, int a) { bits[a >> 3] |= (uint8_t)(1u << (a & 7)); }

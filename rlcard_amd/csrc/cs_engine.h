@@ -89,6 +89,26 @@ hipError_t np10_launch_step(const Buffers& b, const int32_t* actions, const cs_s
 hipError_t np10_launch_observe(const Buffers& b, int32_t player, const cs_step_out& o, hipStream_t s);
 hipError_t np10_launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
                                const cs_traj_out& o, hipStream_t s);
+// cs_holdem_n16.hip: the same for 11..16 players
+int np16_game_info(int32_t game, int32_t num_players, cs_game_info* info);
+int64_t np16_stage_bytes(int32_t game, int32_t num_players);
+hipError_t np16_launch_seed(const Buffers& b, const uint32_t* keys_dev, const int32_t* klen_dev, int64_t first,
+                            int64_t count, hipStream_t s);
+hipError_t np16_launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s);
+hipError_t np16_launch_step(const Buffers& b, const int32_t* actions, const cs_step_out& o, hipStream_t s);
+hipError_t np16_launch_observe(const Buffers& b, int32_t player, const cs_step_out& o, hipStream_t s);
+hipError_t np16_launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
+                               const cs_traj_out& o, hipStream_t s);
+// cs_holdem_n22.hip: the same for 17..22 players
+int np22_game_info(int32_t game, int32_t num_players, cs_game_info* info);
+int64_t np22_stage_bytes(int32_t game, int32_t num_players);
+hipError_t np22_launch_seed(const Buffers& b, const uint32_t* keys_dev, const int32_t* klen_dev, int64_t first,
+                            int64_t count, hipStream_t s);
+hipError_t np22_launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s);
+hipError_t np22_launch_step(const Buffers& b, const int32_t* actions, const cs_step_out& o, hipStream_t s);
+hipError_t np22_launch_observe(const Buffers& b, int32_t player, const cs_step_out& o, hipStream_t s);
+hipError_t np22_launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
+                               const cs_traj_out& o, hipStream_t s);
 // cs_blackjack_shoe.hip: Blackjack with 2..8-deck shoes or 5..7 players (word-stream RNG, materialised shoe)
 bool is_blackjack_shoe(const Buffers& b);
 int bjs_game_info(const cs_config* cfg, cs_game_info* info);

@@ -1,4 +1,4 @@
-// cs_holdem_n.h -- Leduc / Limit / No-limit hold'em with 3..10 players (Leduc 3..5) ('game_num_players', envs/env.py:33-39), as
+// cs_holdem_n.h -- Leduc / Limit / No-limit hold'em with 3..22 players (Leduc 3..5) ('game_num_players', envs/env.py:33-39), as
 // lane-per-env lockstep state machines over the shared skeleton (cs_skeleton.h). The heads-up games keep their
 // specialised kernels (cs_leduc.h, cs_limit.h, cs_nolimit.h); these follow the reference's per-player loops directly.
 //
@@ -343,18 +343,18 @@ struct LeducN {
     }
 };
 
-// ---- Limit Texas Hold'em, P = 3..10 ----------------------------------------------------------------------------------
+// ---- Limit Texas Hold'em, P = 3..22 ----------------------------------------------------------------------------------
 // player word: c0:6 c1:6 in:8 (12) raised:6 (20) folded:1 (26)
-// S0: board c0..c4 6 bits each; S1: ptr:4 rc:3 (4) have_raised:3 (7) not_raise_num:4 (10) use_prev:1 (14) over:1 (31)
+// S0: board c0..c4 6 bits each; S1: ptr:5 rc:3 (5) have_raised:3 (8) not_raise_num:5 (11) use_prev:1 (16) over:1 (31)
 // S2: raise_nums 4 x 3 (0..11), prev_raise_nums 4 x 3 (12..23) (the reset obs shows the previous game's, game.py:98)
 template <int NP>
 struct LimitN {
-    static_assert(NP >= 3 && NP <= 10, "limit: 3..10 players");
+    static_assert(NP >= 3 && NP <= 22, "limit: 3..22 players (2P + 5 <= 52 dealt cards)");
     static constexpr int OBS = 72, A = 4, P = NP, LB = 1, WORDS = NP + 3, ACTION_BYTES = 1, NB = 3;
     static constexpr bool RING = true, RAW_OBS = false, PAYOFF_DRAWS = true;
     static constexpr int SCRATCH_WORDS = 0;
     static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_PAD = 8, STAGE_R = 100, STAGE_RF = 120;
-    static constexpr int RESTAGE_B = 8, MIN_WAVES = 3, EPW = 64, REFILL_K = 2;
+    static constexpr int RESTAGE_B = 8, MIN_WAVES = NP <= 10 ? 3 : 2, EPW = 64, REFILL_K = 2;
     enum { CALL = 0, RAISE = 1, FOLD = 2, CHECK = 3 };
     __device__ __forceinline__ void bind(uint32_t*, const GameParams&) {}
 
@@ -379,7 +379,7 @@ struct LimitN {
         for (int i = 0; i < NP; i++) pw.w[i] = 0;
         s0 = 0; s1 = 1u << 31; s2 = 0;
     }
-    __device__ __forceinline__ int current() const { return (int)bf(s1, 0, 4); }
+    __device__ __forceinline__ int current() const { return (int)bf(s1, 0, 5); }
     __device__ __forceinline__ bool is_over() const { return (s1 >> 31) != 0; }
     __device__ __forceinline__ int max_raised() const
     {
@@ -393,7 +393,7 @@ struct LimitN {
     {
         const int mx = max_raised(), rp = (int)bf(pw.get(current()), 20, 6);
         uint32_t m = 0xF;
-        if (bf(s1, 7, 3) >= 4) m &= ~(1u << RAISE);
+        if (bf(s1, 8, 3) >= 4) m &= ~(1u << RAISE);
         if (rp < mx) m &= ~(1u << CHECK);
         if (rp == mx) m &= ~(1u << CALL);
         return m;
@@ -402,14 +402,14 @@ struct LimitN {
     __device__ __forceinline__ void observe(int player, uint32_t (&bits)[NB]) const
     {
         bits[0] = bits[1] = bits[2] = 0;
-        const int r = (int)bf(s1, 4, 3), npub = r == 0 ? 0 : (r == 1 ? 3 : (r == 2 ? 4 : 5));
+        const int r = (int)bf(s1, 5, 3), npub = r == 0 ? 0 : (r == 1 ? 3 : (r == 2 ? 4 : 5));
 #pragma unroll
         for (int k = 0; k < 5; k++)
             if (k < npub) set_bit(bits, (int)bf(s0, 6 * k, 6));
         const uint32_t me = pw.get(player);
         set_bit(bits, (int)bf(me, 0, 6));
         set_bit(bits, (int)bf(me, 6, 6));
-        const uint32_t rn = bf(s1, 14, 1) ? (s2 >> 12) : s2;
+        const uint32_t rn = bf(s1, 16, 1) ? (s2 >> 12) : s2;
 #pragma unroll
         for (int i = 0; i < 4; i++) set_bit(bits, 52 + 5 * i + (int)((rn >> (3 * i)) & 7u));
     }
@@ -428,7 +428,7 @@ struct LimitN {
         s0 = 0;
 #pragma unroll
         for (int k = 0; k < 5; k++) s0 |= d[2 * NP + k] << (6 * k);
-        s1 = (uint32_t)next_seat<NP>(bb) | 1u << 14;                    // first actor BB + 1; use_prev
+        s1 = (uint32_t)next_seat<NP>(bb) | 1u << 16;                    // first actor BB + 1; use_prev
         s2 = (s2 & 0xFFFu) << 12;                                       // prev <- current, current <- 0
     }
 
@@ -437,8 +437,8 @@ struct LimitN {
     {
         const uint32_t lg = legal();
         if (a < 0 || a > 3 || !((lg >> a) & 1u)) a = ((lg >> CHECK) & 1u) ? CHECK : FOLD;
-        const int p = current(), mx = max_raised(), rc = (int)bf(s1, 4, 3);
-        int hr = (int)bf(s1, 7, 3), nrn = (int)bf(s1, 10, 4);
+        const int p = current(), mx = max_raised(), rc = (int)bf(s1, 5, 3);
+        int hr = (int)bf(s1, 8, 3), nrn = (int)bf(s1, 11, 5);
         uint32_t w = pw.get(p);
         const int rp = (int)bf(w, 20, 6), ra = rc >= 2 ? 4 : 2;
         if (a == CALL) { w = bf_set(w, 12, 8, bf(w, 12, 8) + (uint32_t)(mx - rp)); w = bf_set(w, 20, 6, mx); nrn += 1; }
@@ -461,7 +461,7 @@ struct LimitN {
 #pragma unroll
         for (int i = 0; i < NP; i++) alive += (int)(((pw.w[i] >> 26) & 1u) ^ 1u);
         const uint32_t over = alive == 1 || r >= 4;
-        s1 = (uint32_t)q | (uint32_t)r << 4 | (uint32_t)hr << 7 | (uint32_t)nrn << 10 | over << 31;   // use_prev cleared
+        s1 = (uint32_t)q | (uint32_t)r << 5 | (uint32_t)hr << 8 | (uint32_t)nrn << 11 | over << 31;   // use_prev cleared
     }
 
     template <class Rng>
@@ -493,18 +493,18 @@ struct LimitN {
     }
 };
 
-// ---- No-limit Texas Hold'em, P = 3..10 -------------------------------------------------------------------------------
+// ---- No-limit Texas Hold'em, P = 3..22 -------------------------------------------------------------------------------
 // player word: c0:6 c1:6 in:8 (12) raised:8 (20) status:2 (28; 0 alive, 1 folded, 2 all-in)
-// S0: board c0..c4 6 bits each; S1: ptr:4 rc:3 (4) not_raise_num:8 (7) not_playing_num:8 (15) dealer:4 (23)
-//     dealer drawn:1 (27) over:1 (31). The stack is chips_for_each - in (not stored).
+// S0: board c0..c4 6 bits each; S1: ptr:5 rc:3 (5) not_raise_num:8 (8) not_playing_num:8 (16) dealer:5 (24)
+//     dealer drawn:1 (29) over:1 (31). The stack is chips_for_each - in (not stored).
 template <int NP>
 struct NolimitN {
-    static_assert(NP >= 3 && NP <= 10, "no-limit: 3..10 players");
+    static_assert(NP >= 3 && NP <= 22, "no-limit: 3..22 players (2P + 5 <= 52 dealt cards)");
     static constexpr int OBS = 54, A = 5, P = NP, LB = 1, WORDS = NP + 2, ACTION_BYTES = 1, NB = 14;
     static constexpr bool RING = true, RAW_OBS = true, PAYOFF_DRAWS = true;
     static constexpr int SCRATCH_WORDS = 0;
     static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_PAD = 8, STAGE_R = 100, STAGE_RF = 100;
-    static constexpr int RESTAGE_B = 8, MIN_WAVES = 3, EPW = 64, REFILL_K = 2;
+    static constexpr int RESTAGE_B = 8, MIN_WAVES = NP <= 10 ? 3 : 2, EPW = 64, REFILL_K = 2;
     enum { FOLD = 0, CHECK_CALL = 1, RAISE_HALF_POT = 2, RAISE_POT = 3, ALL_IN = 4 };
     enum { ALIVE = 0, FOLDED = 1, ALLIN = 2 };
 
@@ -535,7 +535,7 @@ struct NolimitN {
         for (int i = 0; i < NP; i++) pw.w[i] = 0;
         s0 = 0; s1 = 1u << 31;
     }
-    __device__ __forceinline__ int current() const { return (int)bf(s1, 0, 4); }
+    __device__ __forceinline__ int current() const { return (int)bf(s1, 0, 5); }
     __device__ __forceinline__ bool is_over() const { return (s1 >> 31) != 0; }
     __device__ __forceinline__ int max_raised() const
     {
@@ -571,7 +571,7 @@ struct NolimitN {
     __device__ __forceinline__ void observe(int player, uint32_t (&raw)[NB]) const
     {
         uint64_t cards = 0;
-        const int r = (int)bf(s1, 4, 3), npub = r == 0 ? 0 : (r + 2 < 5 ? r + 2 : 5);
+        const int r = (int)bf(s1, 5, 3), npub = r == 0 ? 0 : (r + 2 < 5 ? r + 2 : 5);
 #pragma unroll
         for (int k = 0; k < 5; k++)
             if (k < npub) cards |= 1ull << bf(s0, 6 * k, 6);
@@ -591,7 +591,7 @@ struct NolimitN {
     {
         int dealer;   // randint(0, N) by the first game when configured None, then kept (game.py:62-63)
         if (dealer_cfg >= 0) dealer = dealer_cfg;
-        else if (bf(s1, 27, 1)) dealer = (int)bf(s1, 23, 4);
+        else if (bf(s1, 29, 1)) dealer = (int)bf(s1, 24, 5);
         else dealer = (int)rng.interval((uint32_t)(NP - 1));
         uint32_t d[2 * NP + 5];
         holdem_deal_k<2 * NP + 5>(rng, d);
@@ -605,7 +605,7 @@ struct NolimitN {
         s0 = 0;
 #pragma unroll
         for (int k = 0; k < 5; k++) s0 |= d[2 * NP + k] << (6 * k);
-        s1 = (uint32_t)next_seat<NP>(bb) | (uint32_t)dealer << 23 | 1u << 27;
+        s1 = (uint32_t)next_seat<NP>(bb) | (uint32_t)dealer << 24 | 1u << 29;
     }
 
     template <class Rng>
@@ -614,7 +614,7 @@ struct NolimitN {
         const uint32_t lg = legal();
         if (a < 0 || a > 4 || !((lg >> a) & 1u)) a = CHECK_CALL;
         const int p = current(), mx = max_raised(), pt = pot();
-        int r = (int)bf(s1, 4, 3), nrn = (int)bf(s1, 7, 8), npn = (int)bf(s1, 15, 8);
+        int r = (int)bf(s1, 5, 3), nrn = (int)bf(s1, 8, 8), npn = (int)bf(s1, 16, 8);
         uint32_t w = pw.get(p);
         int ip = (int)bf(w, 12, 8), rp = (int)bf(w, 20, 8), sp = (int)bf(w, 28, 2);
         int want = 0;   // chips asked for; bet() clamps to the stack
@@ -645,7 +645,7 @@ struct NolimitN {
         }
         if (NP - nby == 1 && (int)bf(pw.get(last), 20, 8) >= max_raised()) { by |= 1u << last; nby += 1; }
         if (nrn + npn >= NP) {   // round over: pointer dealer + 1 past bypassed players (unless all are), deal
-            int g = next_seat<NP>((int)bf(s1, 23, 4));
+            int g = next_seat<NP>((int)bf(s1, 24, 5));
             if (nby < NP) {
 #pragma unroll
                 for (int k = 0; k < NP; k++)
@@ -661,8 +661,8 @@ struct NolimitN {
 #pragma unroll
         for (int i = 0; i < NP; i++) in_hand += bf(pw.w[i], 28, 2) != FOLDED ? 1 : 0;
         const uint32_t over = in_hand == 1 || r >= 4;
-        s1 = (uint32_t)q | (uint32_t)r << 4 | (uint32_t)(nrn & 255) << 7 | (uint32_t)(npn & 255) << 15 |
-             (s1 & (0x1Fu << 23)) | over << 31;
+        s1 = (uint32_t)q | (uint32_t)r << 5 | (uint32_t)(nrn & 255) << 8 | (uint32_t)(npn & 255) << 16 |
+             (s1 & (0x3Fu << 24)) | over << 31;
     }
 
     template <class Rng>

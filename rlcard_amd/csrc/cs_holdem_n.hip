@@ -1,6 +1,6 @@
-// cs_holdem_n.hip -- the lockstep skeleton (cs_skeleton.h) instantiated for 3..10-player hold'em (cs_holdem_n.h):
-// Leduc 3..5, Limit and No-limit 3..6 here; 7..10 in cs_holdem_n10.hip (its own translation unit: the two compile in
-// parallel). Reached from the dispatch in cs_kernels.hip when cs_config.num_players > 2.
+// cs_holdem_n.hip -- the lockstep skeleton (cs_skeleton.h) instantiated for 3..22-player hold'em (cs_holdem_n.h):
+// Leduc 3..5, Limit and No-limit 3..6 here; 7..10, 11..16 and 17..22 in cs_holdem_n10.hip / n16.hip / n22.hip (their
+// own translation units: they compile in parallel). Reached from the dispatch in cs_kernels.hip when cs_config.num_players > 2.
 #include "cs_skeleton.h"
 #include "cs_holdem_n.h"
 
@@ -42,13 +42,15 @@ bool np_supported(int32_t game, int32_t np)
     switch (game) {
     case CS_GAME_LEDUC: return np >= 3 && np <= 5;
     case CS_GAME_LIMIT:
-    case CS_GAME_NOLIMIT: return np >= 3 && np <= 10;
+    case CS_GAME_NOLIMIT: return np >= 3 && np <= 22;
     default: return false;
     }
 }
 
 int np_game_info(int32_t game, int32_t np, cs_game_info* info)
 {
+    if (np > 16) return np22_game_info(game, np, info);
+    if (np > 10) return np16_game_info(game, np, info);
     if (np > 6) return np10_game_info(game, np, info);
 #define C_(G) (fill_info<G>(info), CS_OK)
     CS_NP_DISPATCH(game, np, C_)
@@ -58,6 +60,8 @@ int np_game_info(int32_t game, int32_t np, cs_game_info* info)
 
 int64_t np_stage_bytes(int32_t game, int32_t np)
 {
+    if (np > 16) return np22_stage_bytes(game, np);
+    if (np > 10) return np16_stage_bytes(game, np);
     if (np > 6) return np10_stage_bytes(game, np);
 #define C_(G) stage_bytes_of<G>()
     CS_NP_DISPATCH(game, np, C_)
@@ -68,6 +72,8 @@ int64_t np_stage_bytes(int32_t game, int32_t np)
 hipError_t np_launch_seed(const Buffers& b, const uint32_t* keys, const int32_t* klen, int64_t first, int64_t count,
                           hipStream_t s)
 {
+    if (b.num_players > 16) return np22_launch_seed(b, keys, klen, first, count, s);
+    if (b.num_players > 10) return np16_launch_seed(b, keys, klen, first, count, s);
     if (b.num_players > 6) return np10_launch_seed(b, keys, klen, first, count, s);
 #define C_(G) seed_g<G>(b, keys, klen, first, count, s)
     CS_NP_DISPATCH(b.game, b.num_players, C_)
@@ -76,6 +82,8 @@ hipError_t np_launch_seed(const Buffers& b, const uint32_t* keys, const int32_t*
 }
 hipError_t np_launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s)
 {
+    if (b.num_players > 16) return np22_launch_reset(b, o, s);
+    if (b.num_players > 10) return np16_launch_reset(b, o, s);
     if (b.num_players > 6) return np10_launch_reset(b, o, s);
 #define C_(G) reset_g<G>(b, o, s)
     CS_NP_DISPATCH(b.game, b.num_players, C_)
@@ -84,6 +92,8 @@ hipError_t np_launch_reset(const Buffers& b, const cs_step_out& o, hipStream_t s
 }
 hipError_t np_launch_step(const Buffers& b, const int32_t* a, const cs_step_out& o, hipStream_t s)
 {
+    if (b.num_players > 16) return np22_launch_step(b, a, o, s);
+    if (b.num_players > 10) return np16_launch_step(b, a, o, s);
     if (b.num_players > 6) return np10_launch_step(b, a, o, s);
 #define C_(G) step_g<G>(b, a, o, s)
     CS_NP_DISPATCH(b.game, b.num_players, C_)
@@ -92,6 +102,8 @@ hipError_t np_launch_step(const Buffers& b, const int32_t* a, const cs_step_out&
 }
 hipError_t np_launch_observe(const Buffers& b, int32_t p, const cs_step_out& o, hipStream_t s)
 {
+    if (b.num_players > 16) return np22_launch_observe(b, p, o, s);
+    if (b.num_players > 10) return np16_launch_observe(b, p, o, s);
     if (b.num_players > 6) return np10_launch_observe(b, p, o, s);
 #define C_(G) observe_g<G>(b, p, o, s)
     CS_NP_DISPATCH(b.game, b.num_players, C_)
@@ -101,6 +113,8 @@ hipError_t np_launch_observe(const Buffers& b, int32_t p, const cs_step_out& o, 
 hipError_t np_launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
                              const cs_traj_out& o, hipStream_t s)
 {
+    if (b.num_players > 16) return np22_launch_rollout(b, T, seed, t0, env_base, o, s);
+    if (b.num_players > 10) return np16_launch_rollout(b, T, seed, t0, env_base, o, s);
     if (b.num_players > 6) return np10_launch_rollout(b, T, seed, t0, env_base, o, s);
 #define C_(G) rollout_g<G>(b, T, seed, t0, env_base, o, s)
     CS_NP_DISPATCH(b.game, b.num_players, C_)

@@ -27,15 +27,15 @@ class LimitholdemEnv(Env):
         return self.actions[action_id]
 
     def _fields(self):
-        if self.num_players > 2:   # cs_holdem_n.h LimitN: a word per player (c0 c1 in:8@12), board, ptr/rc, raises
+        if self.num_players > 2:   # cs_holdem_n.h LimitN: a word per player (c0 c1 in:8@12), board, ptr:5 rc:3@5, raises
             w = self._state_words()
             P = self.num_players
             b, s1, s2 = w[P], w[P + 1], w[P + 2]
-            rc = (s1 >> 4) & 7
+            rc = (s1 >> 5) & 7
             nboard = 0 if rc == 0 else min(5, rc + 2)
-            rn = (s2 >> 12) if (s1 >> 14) & 1 else s2
+            rn = (s2 >> 12) if (s1 >> 16) & 1 else s2
             return dict(hands=[[x & 63, (x >> 6) & 63] for x in w[:P]], board=[(b >> (6 * k)) & 63 for k in range(nboard)],
-                        chips=[(x >> 12) & 255 for x in w[:P]], ptr=s1 & 15, rc=rc,
+                        chips=[(x >> 12) & 255 for x in w[:P]], ptr=s1 & 31, rc=rc,
                         raise_nums=[(rn >> (3 * k)) & 7 for k in range(4)])
         w0, w1, w2, w3 = self._state_words()[:4]
         rc = (w2 >> 21) & 7

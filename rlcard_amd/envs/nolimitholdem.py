@@ -50,15 +50,15 @@ class NolimitholdemEnv(Env):
 
     def _fields(self):
         stack = int(self.game_config['chips_for_each'])
-        if self.num_players > 2:   # cs_holdem_n.h NolimitN: a word per player (c0 c1 in:8@12), board, ptr/rc
+        if self.num_players > 2:   # cs_holdem_n.h NolimitN: a word per player (c0 c1 in:8@12), board, ptr:5 rc:3@5
             w = self._state_words()
             P = self.num_players
             b, s1 = w[P], w[P + 1]
-            rc = (s1 >> 4) & 7
+            rc = (s1 >> 5) & 7
             nboard = 0 if rc == 0 else min(5, rc + 2)
             chips = [(x >> 12) & 255 for x in w[:P]]
             return dict(hands=[[x & 63, (x >> 6) & 63] for x in w[:P]], board=[(b >> (6 * k)) & 63 for k in range(nboard)],
-                        chips=chips, stakes=[stack - c for c in chips], ptr=s1 & 15, rc=rc)
+                        chips=chips, stakes=[stack - c for c in chips], ptr=s1 & 31, rc=rc)
         w0, w1, w2, w3 = self._state_words()[:4]
         rc = (w0 >> 27) & 7
         nboard = 0 if rc == 0 else min(5, rc + 2)

@@ -17,7 +17,7 @@ import torch
 import torch.distributed as dist
 
 __all__ = ['shard_range', 'ShardedVecEnv', 'gather_traj', 'gather_traj_to', 'new_gathered', 'rank_max',
-           'whole_job_rate', 'traj_bytes', 'time_exchange']
+           'whole_job_rate', 'traj_bytes', 'time_exchange', 'shard_digest', 'verify_gathered']
 
 
 def shard_range(envs_per_rank, rank):
@@ -68,6 +68,40 @@ def gather_traj_to(traj, out, dst=0, group=None):
     return out if rank == dst else None
 
 
+def shard_digest(traj):
+    """A position-sensitive fingerprint of a trajectory shard, computed where it lives: per tensor (sorted keys), the
+    wrapping int64 sums of its bytes in 4 KiB blocks (the last block zero-padded). Equal digests on sender and receiver
+    mean the slice arrived intact and in its place."""
+    parts = []
+    for k in sorted(traj):
+        v = traj[k].contiguous().view(-1).view(torch.uint8)
+        main = v.numel() // 4096 * 4096
+        if main:
+            parts.append(v[:main].view(torch.int64).view(-1, 512).sum(dim=1))
+        if v.numel() > main:
+            tail = torch.zeros(4096, dtype=torch.uint8, device=v.device)
+            tail[:v.numel() - main] = v[main:]
+            parts.append(tail.view(torch.int64).sum().reshape(1))
+    return torch.cat(parts)
+
+
+def verify_gathered(traj, gathered, group=None):
+    """After an exchange: every rank's digest of its own shard goes to every rank (a small all-gather), each rank
+    holding gathered buffers checks every slice r against rank r's digest, and the verdict is the AND over ranks."""
+    world = dist.get_world_size(group)
+    mine = shard_digest(traj)
+    digests = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(digests, mine, group=group)
+    ok = True
+    if gathered is not None:
+        for r in range(world):
+            got = shard_digest({k: v[r] for k, v in gathered.items()})
+            ok = ok and bool(torch.equal(got, digests[r]))
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=mine.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    return bool(flag.item())
+
+
 def rank_max(x, device=None, group=None):
     """max over ranks of a host float (a per-rank elapsed time); x itself with one rank."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
@@ -108,6 +142,8 @@ def time_exchange(produce, traj, mode, steps, envs_per_rank, steps_per_launch, s
                 steps=steps, ms_per_step=1e3 * el / steps,
                 value=whole_job_rate(envs_per_rank, steps_per_launch, steps, el, world),
                 bytes_per_rank_per_step=traj_bytes(traj))
+    # untimed: the last exchange's slices checked against their senders' digests (shard_digest)
+    info['verified'] = verify_gathered(traj, gathered)
     return info, gathered
 
 

@@ -266,11 +266,12 @@ def drive_np(env_id, cfgs, seeds, games, stream):
 
 def gen_nplayer():
     specs = [('leduc-holdem', 'leduc_np', 36, 4, [3, 3, 4, 4, 5, 5], [{}] * 6, 40),
-             ('limit-holdem', 'limit_np', 72, 4, [3, 3, 4, 5, 6, 6, 8, 10], [{}] * 8, 30),
-             ('no-limit-holdem', 'nolimit_np', 54, 5, [3, 3, 4, 4, 6, 6, 3, 4, 6, 8, 10, 9],
+             ('limit-holdem', 'limit_np', 72, 4, [3, 3, 4, 5, 6, 6, 8, 10, 12, 16, 22], [{}] * 11, 30),
+             ('no-limit-holdem', 'nolimit_np', 54, 5, [3, 3, 4, 4, 6, 6, 3, 4, 6, 8, 10, 9, 12, 17, 22],
               [{}] * 6 + [{'chips_for_each': 10}, {'chips_for_each': 6, 'dealer_id': 2},
                           {'chips_for_each': 20, 'dealer_id': 5}, {}, {'chips_for_each': 15},
-                          {'chips_for_each': 8, 'dealer_id': 7}], 40)]
+                          {'chips_for_each': 8, 'dealer_id': 7}, {}, {'chips_for_each': 12, 'dealer_id': 16},
+                          {'chips_for_each': 30}], 40)]
     for env_id, name, O, A, nps, extra, games in specs:
         seeds = [11 + 17 * i for i in range(len(nps))]
         cfgs = [dict(e, game_num_players=n) for n, e in zip(nps, extra)]

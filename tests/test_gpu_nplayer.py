@@ -1,4 +1,4 @@
-"""3..10-player hold'em ('game_num_players') on the HIP engine vs the reference streams and the CPU oracle, through the
+"""3..22-player hold'em ('game_num_players') on the HIP engine vs the reference streams and the CPU oracle, through the
 C ABI. Needs a GPU. Kernels: rlcard_amd/csrc/cs_holdem_n.h; oracle: oracle/or_leduc.c, or_limit.c, or_nolimit.c,
 or_judger.c; fixtures: tests/golden/*_np.npz (tests/golden/gen_golden.py --only nplayer)."""
 import numpy as np
@@ -14,7 +14,9 @@ FIXTURES = [('leduc-holdem', 'leduc_np'), ('limit-holdem', 'limit_np'), ('no-lim
 CASES = [('leduc-holdem', 3, {}), ('leduc-holdem', 5, {}), ('limit-holdem', 3, {}), ('limit-holdem', 6, {}),
          ('no-limit-holdem', 4, {}), ('no-limit-holdem', 6, {'chips_for_each': 10}),
          ('no-limit-holdem', 3, {'chips_for_each': 6, 'dealer_id': 2}), ('limit-holdem', 10, {}),
-         ('no-limit-holdem', 8, {'chips_for_each': 15}), ('no-limit-holdem', 10, {'dealer_id': 9})]
+         ('no-limit-holdem', 8, {'chips_for_each': 15}), ('no-limit-holdem', 10, {'dealer_id': 9}),
+         ('limit-holdem', 12, {}), ('limit-holdem', 22, {}), ('no-limit-holdem', 16, {'chips_for_each': 20}),
+         ('no-limit-holdem', 22, {'dealer_id': 21})]
 
 
 def _np(o):
@@ -114,7 +116,8 @@ def test_nplayer_rollout_matches_oracle(oracle, game, players, cfg, flags):
         assert v.rng_position(i) == ob.draws(i) % v.rng_period
 
 
-@pytest.mark.parametrize('game,players', [('leduc-holdem', 4), ('limit-holdem', 5), ('no-limit-holdem', 6)])
+@pytest.mark.parametrize('game,players', [('leduc-holdem', 4), ('limit-holdem', 5), ('no-limit-holdem', 6),
+                                          ('limit-holdem', 22), ('no-limit-holdem', 17)])
 def test_nplayer_compat_env(game, players):
     """rlcard_amd.make with game_num_players: shapes, raw_obs decoding of the N-player state words, Env.run."""
     import rlcard_amd

@@ -133,9 +133,15 @@ def _worker_exchange(rank, world, port, q):
             info, g = time_exchange(produce, traj, mode, 3, 8, 4)
             held = None if g is None else {k: v.clone() for k, v in g.items()}
             res[mode] = (info, held)
+        # a corrupted slice on the receiving side fails verification on every rank
+        info, g = time_exchange(produce, traj, 'all', 1, 8, 4)
+        from rlcard_amd.shard import verify_gathered
+        g['obs'][1 - rank, 2, 3, 1] += 1
+        corrupt_ok = verify_gathered(traj, g)
         q.put((rank, calls[0], {m: (i['mode'], i['steps'], i['value'] > 0, i['bytes_per_rank_per_step'],
-                                    None if h is None else (h['obs'][:, 0, 0, 0].tolist(), h['reward'].shape))
-                                for m, (i, h) in res.items()}))
+                                    None if h is None else (h['obs'][:, 0, 0, 0].tolist(), h['reward'].shape),
+                                    i['verified'])
+                                for m, (i, h) in res.items()}, info['verified'], corrupt_ok))
     finally:
         dist.destroy_process_group()
 
@@ -147,16 +153,48 @@ def test_two_rank_exchange_phase_of_bench():
     procs = [ctx.Process(target=_worker_exchange, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict((r, (c, m)) for r, c, m in [q.get(timeout=240) for _ in range(2)])
+    res = dict((r, (c, m, v, bad)) for r, c, m, v, bad in [q.get(timeout=240) for _ in range(2)])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     for r in (0, 1):
-        calls, m = res[r]
-        assert calls == 6
+        calls, m, v, bad = res[r]
+        assert m['rank0'][5] and m['all'][5] and v, 'exchanged shards verified against their senders'
+        assert not bad, 'a corrupted slice fails verification'
+        assert calls == 7   # 3 + 3 exchanges, then the corrupted-slice round
         assert m['rank0'][:3] == ('rank0', 3, True) and m['all'][:3] == ('all', 3, True)
         assert m['rank0'][3] == 4 * 8 * 3 + 4 * 8 * 2 * 4
         # the last exchange of each mode holds every rank's last shard: rank r's obs = 10 r + call number
         assert m['all'][4] == ([3 + 3, 13 + 3], (2, 4, 8, 2))
     assert res[0][1]['rank0'][4] == ([3, 13], (2, 4, 8, 2))
     assert res[1][1]['rank0'][4] is None
+
+
+@pytest.mark.gpu
+def test_nccl_world1_exchange_on_device_trajectories():
+    """bench.py's exchange phase over RCCL on the GPU (world size 1: the all_gather_into_tensor call on the uint8 /
+    int16 / f32 trajectory tensors of a real DouDizhu rollout and the rank-0 copy path), with the shard verification.
+    8-GPU runs are the driver's; this makes the RCCL calls run on hardware at least once."""
+    if not torch.cuda.is_available():
+        pytest.fail('GPU tests need a visible GPU')
+    port = _free_port()
+    dist.init_process_group('nccl', init_method='tcp://127.0.0.1:%d' % port, rank=0, world_size=1,
+                            device_id=torch.device('cuda', 0))
+    try:
+        from rlcard_amd.shard import ShardedVecEnv, time_exchange
+        env = ShardedVecEnv('doudizhu', 96, 0, seed=42, device=0)
+        env.reset()
+        traj = env.new_traj_out(8)
+        t = [0]
+
+        def produce():
+            env.rollout(8, policy_seed=5, t0=8 * t[0], out=traj)
+            t[0] += 1
+        assert traj['action'].dtype == torch.int16 and traj['obs'].dtype == torch.uint8
+        for mode in ('rank0', 'all'):
+            info, g = time_exchange(produce, traj, mode, 2, 96, 8, torch.cuda.synchronize, torch.device('cuda', 0))
+            assert info['verified'] and info['value'] > 0
+            for k, v in traj.items():
+                assert torch.equal(g[k][0], v), (mode, k)
+    finally:
+        dist.destroy_process_group()

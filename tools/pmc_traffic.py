@@ -1,5 +1,5 @@
 """Record the HBM traffic and duration of a bench configuration's k_rollout from rocprofv3 runs of bench.py
-(tools/profile.sh: kernel trace + stats, then one --pmc pass each for FETCH_SIZE and WRITE_SIZE) into
+(tools/gpu.sh profile:GAME: kernel trace + stats, then one --pmc pass each for FETCH_SIZE and WRITE_SIZE) into
 profiles/traffic.json, where bench.py reads it for roofline.traffic.
 
 Only the LAST `steps` k_rollout dispatches of each run are used -- bench.py's timed launches -- so the untimed
