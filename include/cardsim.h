@@ -111,7 +111,8 @@ typedef struct {
 int cs_game_info_get(int32_t game, const cs_config* cfg, cs_game_info* info);
 
 /* Create n envs of `game` on HIP device `device`. Replaces rlcard.make(env_id, config) (envs/registration.py:77-89)
- * for n independent envs; allocates state (state_words*4 B/env) + MT19937 streams (4992 B/env) in HBM. */
+ * for n independent envs; allocates state (state_words*4 B/env) + the MT19937 streams in HBM: lane games' byte ring
+ * 12 480 B/env (624 block words + 16 x 624 ring bytes), doudizhu 4 992 B/env, Blackjack shoes 2 496 B/env. */
 int cs_create(cs_handle** out, int32_t game, int64_t num_envs, int32_t device, const cs_config* cfg);
 void cs_destroy(cs_handle* h);
 

@@ -128,10 +128,10 @@ __device__ __forceinline__ uint32_t holdem_rank7_bf(uint64_t smp)
 
 __device__ inline uint32_t holdem_rank7(uint64_t cnt, uint64_t smp)
 {
-    if constexpr (!CS_EVAL_BRANCHY) return holdem_rank7_bf(smp);
 #ifdef CS_PROF_NO_EVAL   // profiling builds only: wrong showdowns, timing of the evaluator
     return (uint32_t)(cnt ^ (cnt >> 32) ^ smp ^ (smp >> 29)) & 0xFFFFFFu;
 #endif
+    if constexpr (!CS_EVAL_BRANCHY) return holdem_rank7_bf(smp);
     const uint32_t sm[4] = {(uint32_t)smp & 0x1FFFu, (uint32_t)(smp >> 16) & 0x1FFFu, (uint32_t)(smp >> 32) & 0x1FFFu,
                             (uint32_t)(smp >> 48) & 0x1FFFu};
     uint32_t m1 = 0, m2 = 0, m3 = 0, m4 = 0;

@@ -139,7 +139,7 @@ class DoudizhuEnv(Env):
         self._removed, self._trace = [], []
         self._check()
 
-    def _after_step(self, player, decoded):
+    def _after_step(self, player, decoded, before):
         self._trace.append((player, decoded))
         removed = []
         if decoded != 'pass':

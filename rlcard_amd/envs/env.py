@@ -191,6 +191,7 @@ class Env(object):
         player = self.get_player_id()
         self.action_recorder.append((player, decoded))
         was_over = bool(self._last['done'])
+        before = self._state_words()
         out = self._call('step', self._action_id(decoded))
         if out['done']:
             self._payoffs = out['reward']
@@ -199,7 +200,7 @@ class Env(object):
             self._payoffs = None
             self._after_deal()
         else:
-            self._after_step(player, decoded)
+            self._after_step(player, decoded, before)
         return self._extract_state(out, out['player'], 'step'), out['player']
 
     def step_back(self):
@@ -306,11 +307,12 @@ class Env(object):
         """The legal ids in the order the reference lists them (ascending for every game but DouDizhu)."""
         return self._legal_ids(out)
 
-    # host-side bookkeeping of raw fields the engine state does not hold (DouDizhu's trace and suit-level hands)
+    # host-side bookkeeping of raw fields the engine state does not hold (DouDizhu's trace and suit-level hands,
+    # No-limit's Python / numpy integer types); `before` = the packed state words the step started from
     def _after_deal(self):
         pass
 
-    def _after_step(self, player, decoded):
+    def _after_step(self, player, decoded, before):
         pass
 
     def _after_step_back(self):

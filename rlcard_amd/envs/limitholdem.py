@@ -40,9 +40,10 @@ class LimitholdemEnv(Env):
         w0, w1, w2, w3 = self._state_words()[:4]
         rc = (w2 >> 21) & 7
         nboard = 0 if rc == 0 else min(5, rc + 2)
+        rn = (w3 >> 12) if (w2 >> 26) & 1 else w3   # a reset state shows the previous game's (game.py:98 / :101)
         return dict(hands=[[w0 & 63, (w0 >> 6) & 63], [(w0 >> 12) & 63, (w0 >> 18) & 63]],
                     board=[(w1 >> (6 * k)) & 63 for k in range(nboard)], chips=[(w0 >> 24) & 63, w2 & 63],
-                    ptr=(w0 >> 30) & 1, rc=rc, raise_nums=[(w3 >> (3 * k)) & 7 for k in range(4)])
+                    ptr=(w0 >> 30) & 1, rc=rc, raise_nums=[(rn >> (3 * k)) & 7 for k in range(4)])
 
     def _raw_obs(self, player_id, legal, via):
         f = self._fields()

@@ -34,6 +34,18 @@ def traj_bytes(traj):
     return sum(v.numel() * v.element_size() for v in traj.values())
 
 
+# dtypes RCCL (NCCL) moves natively; anything else (DouDizhu's int16 action rows) is moved as its bytes
+_NCCL_DTYPES = {torch.uint8, torch.int8, torch.int32, torch.int64, torch.float16, torch.bfloat16, torch.float32,
+                torch.float64}
+
+
+def _wire(t, backend):
+    """t itself, or a uint8 view of its bytes when the backend cannot move its dtype (same memory)."""
+    if backend != 'gloo' and t.dtype not in _NCCL_DTYPES:
+        return t.view(torch.uint8)
+    return t
+
+
 def gather_traj(traj, out, group=None):
     """All-gather every trajectory tensor [T, N, ...] of this rank into out[k] = [world, T, N, ...] (rank-major, so
     out[k][r] is rank r's shard = global envs [r*N, (r+1)*N))."""
@@ -42,7 +54,7 @@ def gather_traj(traj, out, group=None):
         if backend == 'gloo':      # gloo has no all_gather_into_tensor for every dtype: use the list form
             dist.all_gather(list(out[k].unbind(0)), v.contiguous(), group=group)
         else:
-            dist.all_gather_into_tensor(out[k], v.contiguous(), group=group)
+            dist.all_gather_into_tensor(_wire(out[k], backend), _wire(v.contiguous(), backend), group=group)
     return out
 
 
@@ -52,16 +64,17 @@ def gather_traj_to(traj, out, dst=0, group=None):
     senders run concurrently. Returns out on dst, None elsewhere."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
+    backend = dist.get_backend(group)
     ops = []
     if rank == dst:
         for k, v in traj.items():
             out[k][dst].copy_(v)
             for r in range(world):
                 if r != dst:
-                    ops.append(dist.P2POp(dist.irecv, out[k][r], r, group))
+                    ops.append(dist.P2POp(dist.irecv, _wire(out[k][r], backend), r, group))
     else:
         for k, v in traj.items():
-            ops.append(dist.P2POp(dist.isend, v.contiguous(), dst, group))
+            ops.append(dist.P2POp(dist.isend, _wire(v.contiguous(), backend), dst, group))
     if ops:
         for w in dist.batch_isend_irecv(ops):
             w.wait()

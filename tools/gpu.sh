@@ -34,9 +34,9 @@ for step in "$@"; do
   case "${a[0]}" in
     tests)
       if [ -n "${a[1]}" ]; then
-        run 900 "$O/tests.log" python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${a[1]}"
+        run 900 "$O/tests.log" python3 -u -m pytest tests -m gpu --maxfail=15 -v --timeout 300 --timeout-method thread -k "${a[1]}"
       else
-        run 1000 "$O/tests.log" python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+        run 1000 "$O/tests.log" python3 -u -m pytest tests -m gpu --maxfail=15 -v --timeout 300 --timeout-method thread
       fi
       tail -3 "$O/tests.log" ;;
     smoke)
@@ -64,6 +64,13 @@ for step in "$@"; do
       run 300 "$d/bench_fetch.log" rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$d/fetch" -o fetch -- python3 $B
       run 300 "$d/bench_write.log" rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$d/write" -o write -- python3 $B
       grep '^{' "$d/bench_kt.log" | tail -1 ;;
+    vcnt)   # vcnt:GAME:N:T:LIB1[:LIB2..]  instruction counts of k_rollout per library build (one PMC pass each)
+      g=${a[1]}; n=${a[2]}; t=${a[3]}; d=$O/vcnt_$g; mkdir -p "$d"
+      for lib in "${a[@]:4}"; do
+        CARDSIM_LIB=$lib run 240 "$d/$lib.log" rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD --output-format csv -d "$d/$lib" -o p -- python3 tools/ab_rollout.py "$g" "$n" "$t" 0
+        echo "== $lib" >> "$d/summary.txt"; python3 tools/pmc_summary.py "$d/$lib" >> "$d/summary.txt" 2>&1
+      done
+      cat "$d/summary.txt" | grep -A 9 "== \|k_rollout" ;;
     ab)
       run 400 "$O/ab_${a[1]}.log" python3 tools/ab_rollout.py "${a[1]}" "${a[2]}" "${a[3]}" "${a[@]:4}"
       cat "$O/ab_${a[1]}.log" ;;
