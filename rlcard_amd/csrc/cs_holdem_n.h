@@ -496,11 +496,12 @@ struct LimitN {
 // ---- No-limit Texas Hold'em, P = 3..22 -------------------------------------------------------------------------------
 // player word: c0:6 c1:6 in:8 (12) raised:8 (20) status:2 (28; 0 alive, 1 folded, 2 all-in)
 // S0: board c0..c4 6 bits each; S1: ptr:5 rc:3 (5) not_raise_num:8 (8) not_playing_num:8 (16) dealer:5 (24)
-//     dealer drawn:1 (29) over:1 (31). The stack is chips_for_each - in (not stored).
+//     dealer drawn:1 (29) over:1 (31); S2: round pot + 1 (0 = the live pot; cs_nolimit.h round_pot). The stack is
+//     chips_for_each - in (not stored).
 template <int NP>
 struct NolimitN {
     static_assert(NP >= 3 && NP <= 22, "no-limit: 3..22 players (2P + 5 <= 52 dealt cards)");
-    static constexpr int OBS = 54, A = 5, P = NP, LB = 1, WORDS = NP + 2, ACTION_BYTES = 1, NB = 14;
+    static constexpr int OBS = 54, A = 5, P = NP, LB = 1, WORDS = NP + 3, ACTION_BYTES = 1, NB = 14;
     static constexpr bool RING = true, RAW_OBS = true, PAYOFF_DRAWS = true;
     static constexpr int SCRATCH_WORDS = 0;
     static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_PAD = 8, STAGE_R = 100, STAGE_RF = 100;
@@ -510,7 +511,7 @@ struct NolimitN {
 
     int chips, dealer_cfg;
     PlayerWords<NP> pw;
-    uint32_t s0, s1;
+    uint32_t s0, s1, s2;
 
     __device__ __forceinline__ void bind(uint32_t*, const GameParams& prm)
     {
@@ -521,19 +522,19 @@ struct NolimitN {
     {
 #pragma unroll
         for (int i = 0; i < NP; i++) pw.w[i] = st[i * n + env];
-        s0 = st[NP * n + env]; s1 = st[(NP + 1) * n + env];
+        s0 = st[NP * n + env]; s1 = st[(NP + 1) * n + env]; s2 = st[(NP + 2) * n + env];
     }
     __device__ __forceinline__ void store(uint32_t* st, int64_t n, int64_t env) const
     {
 #pragma unroll
         for (int i = 0; i < NP; i++) st[i * n + env] = pw.w[i];
-        st[NP * n + env] = s0; st[(NP + 1) * n + env] = s1;
+        st[NP * n + env] = s0; st[(NP + 1) * n + env] = s1; st[(NP + 2) * n + env] = s2;
     }
     __device__ __forceinline__ void blank()
     {
 #pragma unroll
         for (int i = 0; i < NP; i++) pw.w[i] = 0;
-        s0 = 0; s1 = 1u << 31;
+        s0 = 0; s1 = 1u << 31; s2 = 0;
     }
     __device__ __forceinline__ int current() const { return (int)bf(s1, 0, 5); }
     __device__ __forceinline__ bool is_over() const { return (s1 >> 31) != 0; }
@@ -544,15 +545,15 @@ struct NolimitN {
         for (int i = 0; i < NP; i++) m = max(m, (int)bf(pw.w[i], 20, 8));
         return m;
     }
-    __device__ __forceinline__ int pot() const
+    __device__ __forceinline__ int pot() const   // the pot the round reads: dealer.pot = sum of in_chips, or S2
     {
         int t = 0;
 #pragma unroll
         for (int i = 0; i < NP; i++) t += (int)bf(pw.w[i], 12, 8);
-        return t;
+        return s2 ? (int)s2 - 1 : t;
     }
 
-    // round.py:132-165 for the player at the pointer (pot = dealer.pot = sum of in_chips)
+    // round.py:132-165 for the player at the pointer
     __device__ __forceinline__ uint32_t legal() const
     {
         const uint32_t w = pw.get(current());
@@ -606,6 +607,7 @@ struct NolimitN {
 #pragma unroll
         for (int k = 0; k < 5; k++) s0 |= d[2 * NP + k] << (6 * k);
         s1 = (uint32_t)next_seat<NP>(bb) | (uint32_t)dealer << 24 | 1u << 29;
+        s2 = 0;
     }
 
     template <class Rng>

@@ -23,7 +23,13 @@
 //       over (31)
 //   w1: board c0..c4 6 bits each (0..29), showdown win0 / win1 (30, 31; holdem_showdown)
 //   w2: in0:8 in1:8 raised0:8 raised1:8
-//   w3: status0:2 status1:2 (0 alive, 1 folded, 2 all-in), not_raise_num:4 (4..7), not_playing_num:4 (8..11)
+//   w3: status0:2 status1:2 (0 alive, 1 folded, 2 all-in), not_raise_num:4 (4..7), not_playing_num:4 (8..11),
+//       round pot + 1 :13 (12..24; 0 = the live pot, see round_pot)
+// round_pot: Round keeps a reference to the game's Dealer and reads dealer.pot (round.py:37, 93-98, 150-159), which
+// Game.get_state refreshes (game.py:200). Game.step_back restores deep copies of the round and of the dealer made by
+// separate deepcopy calls (game.py:137-143, 219), so from the first step back of a game the round reads a detached
+// dealer whose pot never changes again until the next init_game: the pot of the snapshot it came from. The host writes
+// that value here when it steps back (rlcard_amd/envs/nolimitholdem.py); the kernels only read it.
 #pragma once
 #include "cs_device.h"
 #include "cs_limit.h"
@@ -78,6 +84,11 @@ struct Nolimit {
     __device__ __forceinline__ int in(int p) const { return (w2 >> (8 * p)) & 255; }
     __device__ __forceinline__ int raised(int p) const { return (w2 >> (16 + 8 * p)) & 255; }
     __device__ __forceinline__ int status(int p) const { return (w3 >> (2 * p)) & 3; }
+    __device__ __forceinline__ int round_pot() const   // the pot the round reads (header: round_pot)
+    {
+        const int f = (int)((w3 >> 12) & 0x1FFFu);
+        return f ? f - 1 : in(0) + in(1);
+    }
 
     __device__ __forceinline__ void load(const uint32_t* st, int64_t n, int64_t env)
     {
@@ -96,7 +107,7 @@ struct Nolimit {
     __device__ __forceinline__ uint32_t legal() const
     {
         const int p = ptr(), r0 = raised(0), r1 = raised(1), mx = r0 > r1 ? r0 : r1, rp = p ? r1 : r0;
-        const int rem = chips - in(p), pot = in(0) + in(1), half = pot >> 1, diff = mx - rp;
+        const int rem = chips - in(p), pot = round_pot(), half = pot >> 1, diff = mx - rp;
         uint32_t m = 0x1F;
         if (diff > 0 && diff >= rem) {
             m = (1u << FOLD) | (1u << CHECK_CALL);
@@ -164,7 +175,7 @@ struct Nolimit {
         int p = ptr(), r = rc();
         int i0 = in(0), i1 = in(1), ra0 = raised(0), ra1 = raised(1), s0 = status(0), s1 = status(1);
         int nrn = (w3 >> 4) & 15, npn = (w3 >> 8) & 15;
-        const int mx = ra0 > ra1 ? ra0 : ra1, pot = i0 + i1;
+        const int mx = ra0 > ra1 ? ra0 : ra1, pot = round_pot();
         int ip = p ? i1 : i0, rp = p ? ra1 : ra0, sp = p ? s1 : s0;
         int want = 0;                                    // chips asked for; bet() clamps to the stack
         if (a == CHECK_CALL) { want = mx - rp; rp = mx; nrn += 1; }
@@ -198,7 +209,8 @@ struct Nolimit {
         const int over = (s0 == FOLDED) + (s1 == FOLDED) == 1 || r >= 4;
         w0 = (w0 & 0x06FFFFFFu) | (uint32_t)p << 24 | (uint32_t)r << 27 | (uint32_t)over << 31;
         w2 = (uint32_t)i0 | (uint32_t)i1 << 8 | (uint32_t)ra0 << 16 | (uint32_t)ra1 << 24;
-        w3 = (uint32_t)s0 | (uint32_t)s1 << 2 | (uint32_t)(nrn & 15) << 4 | (uint32_t)(npn & 15) << 8;
+        w3 = (uint32_t)s0 | (uint32_t)s1 << 2 | (uint32_t)(nrn & 15) << 4 | (uint32_t)(npn & 15) << 8 |
+             (w3 & 0x1FFF000u);
     }
 
     __device__ __forceinline__ void payoffs(float (&out)[P]) const

@@ -212,9 +212,11 @@ class Env(object):
         if not self._history:
             return False
         words, last, payoffs = self._history.pop()
+        current = self._state_words()
         gw = self._vec.game_words
         if gw is not None:   # hold'em: the game words only; deals already drawn ahead stay queued
             words = list(words[:gw]) + self._vec.env_state_words(0)[gw:]
+        words = self._step_back_words(list(words), current)
         self._vec.set_env_state_words(0, words)
         self._words = list(words)
         self._last, self._payoffs = last, payoffs
@@ -317,6 +319,11 @@ class Env(object):
 
     def _after_step_back(self):
         pass
+
+    def _step_back_words(self, words, current):
+        """The state words step_back writes: the snapshot, amended where the reference's Game.step_back does not
+        restore everything it saved (limit hold'em's raise history, no-limit's round pot)."""
+        return words
 
     def _legal_value(self, action_id):
         return None

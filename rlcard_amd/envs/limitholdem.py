@@ -45,6 +45,19 @@ class LimitholdemEnv(Env):
                     board=[(w1 >> (6 * k)) & 63 for k in range(nboard)], chips=[(w0 >> 24) & 63, w2 & 63],
                     ptr=(w0 >> 30) & 1, rc=rc, raise_nums=[(rn >> (3 * k)) & 7 for k in range(4)])
 
+    def _step_back_words(self, words, current):
+        """Game.step_back assigns the saved raise history to a misspelt attribute (game.py:167-168,
+        history_raises_nums), so history_raise_nums keeps what the undone steps wrote, and the restored state shows
+        that list, not the previous game's one a reset state shows (use_prev cleared)."""
+        if self.num_players > 2:   # cs_holdem_n.h LimitN: raises in S2 (current 0..11), use_prev S1 bit 16
+            P = self.num_players
+            words[P + 2] = (words[P + 2] & ~0xFFF) | (current[P + 2] & 0xFFF)
+            words[P + 1] &= ~(1 << 16)
+        else:                      # cs_limit.h: raises in w3 (current 0..11), use_prev w2 bit 26
+            words[3] = (words[3] & ~0xFFF) | (current[3] & 0xFFF)
+            words[2] &= ~(1 << 26)
+        return words
+
     def _raw_obs(self, player_id, legal, via):
         f = self._fields()
         return {'hand': [card_str(c) for c in f['hands'][player_id]], 'public_cards': [card_str(c) for c in f['board']],

@@ -85,6 +85,20 @@ class NolimitholdemEnv(Env):
     def _after_step_back(self):
         self._np_in, self._np_rem, self._np_raised = self._np_stack.pop()
 
+    def _step_back_words(self, words, current):
+        """Game.step_back restores deep copies of the round and of the dealer made by separate deepcopy calls
+        (game.py:137-143, 219): the round's dealer is detached from the game's from then on, and the round (legal
+        actions, pot-sized raises, round.py:93-98, 150-159) reads the pot that detached copy holds -- the pot of the
+        snapshot's state, or of the earlier snapshot it was itself restored from -- until the next init_game.
+        The engine keeps that value + 1 in the round-pot field (cs_nolimit.h round_pot; 0 = live pot)."""
+        P = self.num_players
+        if P > 2:
+            if words[P + 2] == 0:
+                words[P + 2] = sum((x >> 12) & 255 for x in words[:P]) + 1
+        elif (words[3] >> 12) & 0x1FFF == 0:
+            words[3] |= ((words[2] & 255) + ((words[2] >> 8) & 255) + 1) << 12
+        return words
+
     def _typed(self, values, numpy_flags):
         return [np.int64(v) if t else int(v) for v, t in zip(values, numpy_flags)]
 

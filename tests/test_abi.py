@@ -65,7 +65,7 @@ def test_invalid_arguments_are_rejected():
 def test_nplayer_game_info():
     """game_num_players 3..22 (Leduc 3..5; 2P + 5 <= 52 dealt cards): same obs / action shapes, one packed word per
     player plus shared words, no deal queue (cs_holdem_n.h); counts past the engine's range are refused."""
-    for game, words_extra, top in (('leduc-holdem', 1, 5), ('limit-holdem', 3, 22), ('no-limit-holdem', 2, 22)):
+    for game, words_extra, top in (('leduc-holdem', 1, 5), ('limit-holdem', 3, 22), ('no-limit-holdem', 3, 22)):
         two, _ = _abi.game_info(game, 2)
         for n in range(3, top + 1):
             info, _ = _abi.game_info(game, n)

@@ -128,13 +128,17 @@ def test_env_run_layout_and_types(game, name):
 @pytest.mark.gpu
 @pytest.mark.parametrize('game,name', GAMES)
 def test_step_back_restores_the_game(game, name):
-    """Env.step_back (env.py:88-108): the state before each step comes back exactly, and for games whose steps draw
-    no cards (all but blackjack) replaying the same actions reproduces the same states."""
+    """Env.step_back (env.py:88-108): the state before each step comes back exactly, and for Leduc and DouDizhu
+    replaying the same actions reproduces the same states. Not for Blackjack (its steps draw cards), nor for the two
+    Texas games, whose reference step_back leaves part of the game behind: limit hold'em keeps the undone steps' raise
+    history (game.py:167-168), no-limit's round reads a detached dealer's pot from then on (game.py:137-143, 219), so
+    raises after a step back can differ; tests/test_raw.py replays the reference's own streams through both."""
     env = rlcard_amd.make(game, config={'seed': 5, 'allow_step_back': True})
     rng = np.random.RandomState(1)
 
-    def snap(s, p):
-        return (p, s['obs'].tobytes(), tuple(s['legal_actions'].keys()))
+    def snap(s, p):   # limit hold'em: the raise-count bits show the list step_back leaves behind (see above)
+        obs = s['obs'][:52] if game == 'limit-holdem' else s['obs']
+        return (p, obs.tobytes(), tuple(s['legal_actions'].keys()))
 
     for _ in range(4):
         state, player = env.reset()
@@ -150,7 +154,7 @@ def test_step_back_restores_the_game(game, name):
             state, player = env.step_back()
             assert snap(state, player) == seen[j - 1] and not env.is_over()
         assert env.step_back() is False
-        if game != 'blackjack':
+        if game in ('leduc-holdem', 'doudizhu'):
             for j, a in enumerate(acts):
                 state, player = env.step(a)
                 assert snap(state, player) == seen[j + 1]
