@@ -119,6 +119,7 @@ __device__ __forceinline__ void mt_twist_wave(const uint32_t* __restrict__ src, 
 // accesses compile to flat_load/flat_store, which count on lgkmcnt too, so every use waits with vmcnt(0) lgkmcnt(0)
 // -- draining the wave's outstanding trajectory stores each time (measured in the k_rollout ISA)
 typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) uint8_t gu8;
 __device__ __forceinline__ gu32* to_global(uint32_t* p) { return (gu32*)p; }
 
 // 64-bit pointer held by lane j (readlane returns int: go through uint32_t so bit 31 of the low half is not
@@ -495,6 +496,18 @@ __device__ __forceinline__ int pick_legal32(uint32_t legal, uint32_t r)
     int k = (int)__umulhi(r, (uint32_t)count);
     while (k--) legal &= legal - 1;
     return __builtin_ctz(legal);
+}
+// the same pick for masks of at most A bits (A <= 8), branch-free: the k-th set bit after k clears of the lowest
+// (k < A), so a wave's lanes never loop to the largest k among them
+template <int A>
+__device__ __forceinline__ int pick_legal_small(uint32_t legal, uint32_t r)
+{
+    static_assert(A >= 1 && A <= 8, "small action sets");
+    const uint32_t count = (uint32_t)__popc(legal);
+    const uint32_t k = __umulhi(r, count);
+#pragma unroll
+    for (uint32_t i = 0; i + 1 < (uint32_t)A; i++) legal = i < k ? legal & (legal - 1u) : legal;
+    return count == 0 ? -1 : __builtin_ctz(legal);
 }
 __device__ __forceinline__ int pick_legal(uint64_t legal, uint32_t r)
 {

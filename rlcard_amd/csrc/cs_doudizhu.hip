@@ -30,7 +30,7 @@ namespace ddz {
 #define CS_DDZ_BLOCK 256
 #endif
 #ifndef CS_DDZ_MINW
-#define CS_DDZ_MINW 1   // k_rollout: minimum waves per SIMD the register allocation must allow
+#define CS_DDZ_MINW 1   // k_rollout: minimum waves per SIMD the register allocation must allow (6 forces 80 VGPRs: slower)
 #endif
 constexpr int BLOCK = CS_DDZ_BLOCK;
 constexpr int WPB = BLOCK / WAVE;
@@ -43,11 +43,14 @@ constexpr int BV_WORDS = 32;                      // obs bits (912 + 16 front pa
 #define CS_PROF_DDZ 0   // profiling only (wrong outputs): 1 skip legal rows, 2 skip obs rows, 4 skip build_obs
 #endif
 
-struct WaveLds {
+constexpr int LIST_RING = 128;                    // the step's tested mask dwords (a ring: see build_legal)
+constexpr int LIST_CAP = 64;                      // kth_legal reads the list when it holds them all, one per lane
+struct alignas(16) WaveLds {
     uint32_t mask[MASK_WORDS];   // legal bits: id i at bit (i & 31) of mask[MASK_PAD + i / 32]
     uint64_t segv[NSEG];         // obs 54-bit blocks
     uint32_t bv[BV_WORDS];       // obs bit x at bit 16 + x
     uint16_t pre[MAX_GROUPS + 8];
+    uint16_t lst[LIST_RING];     // the mask dwords pass c tests this step, ascending (Legal::nl of them)
 };
 
 // the group table and the per-dword group ranges, copied once per block (read by every step's scan)
@@ -346,6 +349,7 @@ __device__ __forceinline__ void deal(Env& e, M& m, int lane)
 // ---- legal mask ------------------------------------------------------------------------------------------------
 struct Legal {
     uint32_t total;   // legal combos (pass not included)
+    uint32_t nl;      // mask dwords pass c tests (listed in L.lst); > LIST_CAP: more, not all listed
 };
 
 __device__ __forceinline__ void zero_mask(WaveLds& L, int lane)
@@ -358,29 +362,28 @@ __device__ __forceinline__ void zero_mask(WaveLds& L, int lane)
     }
 }
 
-// pass c for up to PAIRS x 2 surviving dwords: lanes 0..31 take the even slot of a pair, 32..63 the odd one; all
-// the id loads are issued before the first test (slots < 0 are empty)
+// pass c for 2 x PAIRS listed dwords from list entry t0 on (entries >= nl are empty): lanes 0..31 take the even entry
+// of a pair, 32..63 the odd one; all the id loads are issued before the first test
 constexpr int PAIRS = 4;
-__device__ __forceinline__ void test_dwords(const int (&ds)[2 * PAIRS], uint64_t h, const Cand& c, const Tab& tb,
+__device__ __forceinline__ void test_listed(uint32_t t0, uint32_t nl, uint64_t h, const Cand& c, const Tab& tb,
                                             WaveLds& L, int lane, Legal& r)
 {
     uint64_t cnt[PAIRS];
-    uint32_t id[PAIRS];
-    bool live[PAIRS];
+    uint32_t id[PAIRS], dw[PAIRS];
+    bool live[PAIRS], ent[PAIRS];
 #pragma unroll
     for (int q = 0; q < PAIRS; q++) {
-        const int d = lane < 32 ? ds[2 * q] : ds[2 * q + 1];
-        id[q] = (uint32_t)d * 32u + (uint32_t)(lane & 31);
-        live[q] = d >= 0 && id[q] < (uint32_t)PASS;
+        const uint32_t e = t0 + 2u * (uint32_t)q + (lane < 32 ? 0u : 1u);
+        ent[q] = e < nl;
+        dw[q] = ent[q] ? L.lst[e & (LIST_RING - 1)] : 0u;
+        id[q] = dw[q] * 32u + (uint32_t)(lane & 31);
+        live[q] = ent[q] && id[q] < (uint32_t)PASS;
         cnt[q] = live[q] ? tb.cnt[id[q]] : ~0ull;
     }
 #pragma unroll
     for (int q = 0; q < PAIRS; q++) {
         const uint64_t m = __ballot(live[q] && contains(h, cnt[q]) && c.ok(id[q]));
-        if (lane == 0) {
-            if (ds[2 * q] >= 0) L.mask[MASK_PAD + ds[2 * q]] = (uint32_t)m;
-            if (ds[2 * q + 1] >= 0) L.mask[MASK_PAD + ds[2 * q + 1]] = (uint32_t)(m >> 32);
-        }
+        if ((lane & 31) == 0 && ent[q]) L.mask[MASK_PAD + dw[q]] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
         r.total += (uint32_t)__popcll(m);
     }
 }
@@ -391,6 +394,7 @@ __device__ __forceinline__ Legal build_legal(const Env& e, const Cand& c, const 
 {
     Legal r;
     r.total = 0;
+    r.nl = 0;
     if (e.over()) return r;                                        // game.py:110-128: no actions once over
     const uint64_t h = e.hand(e.cur);
     // a. groups
@@ -409,11 +413,8 @@ __device__ __forceinline__ Legal build_legal(const Env& e, const Cand& c, const 
     }
     if (base == 0) return r;
     wave_sync_lds();
-    // b. dwords that any passing group overlaps; c. their ids, 2 x PAIRS dwords per batch (collected across chunks)
-    int ds[2 * PAIRS];
-#pragma unroll
-    for (int j = 0; j < 2 * PAIRS; j++) ds[j] = -1;
-    int nf = 0;
+    // b. dwords that any passing group overlaps, appended to the list in ascending order (a ring of LIST_RING: at most
+    // 7 + 64 entries wait for their test); c. their ids, 2 x PAIRS listed dwords per batch
     // chunks of 64 dwords that any passing group reaches (lane k tests chunk k): the others are skipped whole
     bool chunk_pass = false;
     if (lane < (ND + WAVE - 1) / WAVE) {
@@ -422,6 +423,7 @@ __device__ __forceinline__ Legal build_legal(const Env& e, const Cand& c, const 
         chunk_pass = L.pre[hi + 1] > L.pre[lo];
     }
     uint64_t chunks = __ballot(chunk_pass);
+    uint32_t tested = 0;
     while (chunks) {
         const int k = __builtin_ctzll(chunks);
         chunks &= chunks - 1;
@@ -431,29 +433,42 @@ __device__ __forceinline__ Legal build_legal(const Env& e, const Cand& c, const 
             const uint32_t dr = T.drange[d];
             pass = L.pre[(dr >> 16) + 1] > L.pre[dr & 0xFFFFu];
         }
-        uint64_t bits = __ballot(pass);
-        while (bits) {
-#pragma unroll
-            for (int j = 0; j < 2 * PAIRS - 1; j++) ds[j] = ds[j + 1];
-            ds[2 * PAIRS - 1] = k * WAVE + __builtin_ctzll(bits);
-            bits &= bits - 1;
-            if (++nf == 2 * PAIRS) {
-                test_dwords(ds, h, c, tb, L, lane, r);
-#pragma unroll
-                for (int j = 0; j < 2 * PAIRS; j++) ds[j] = -1;
-                nf = 0;
-            }
-        }
+        const uint64_t bits = __ballot(pass);
+        if (pass) L.lst[(r.nl + mbcnt(bits)) & (LIST_RING - 1)] = (uint16_t)d;
+        r.nl += (uint32_t)__popcll(bits);
+        for (; r.nl - tested >= 2u * PAIRS; tested += 2u * PAIRS) test_listed(tested, r.nl, h, c, tb, L, lane, r);
     }
-    if (nf) test_dwords(ds, h, c, tb, L, lane, r);
+    if (tested < r.nl) test_listed(tested, r.nl, h, c, tb, L, lane, r);
     return r;
 }
 
-// the k-th legal id in ascending order (k < total + !leading; pass is the largest id): lane l counts the legal bits
-// of mask dwords [16 l, 16 l + 16), a wave prefix scan finds the lane, 16 lanes then find the dword
+// the k-th set bit of `word` (k < popcount): lane l < 32 holds bit l, mbcnt counts the set bits below it
+__device__ __forceinline__ uint32_t kth_bit(uint32_t word, uint32_t k, int lane)
+{
+    const bool hit = lane < 32 && ((word >> (lane & 31)) & 1u) && __builtin_amdgcn_mbcnt_lo(word, 0u) == k;
+    return (uint32_t)__builtin_ctzll(__ballot(hit));
+}
+
+// the k-th legal id in ascending order (k < total + !leading; pass is the largest id). Listed dwords (the usual
+// case): lane l holds listed dword l, one wave prefix scan over their popcounts finds it. Else (list overflow) lane l
+// counts the legal bits of mask dwords [16 l, 16 l + 16), a wave prefix scan finds the lane, 16 lanes then the dword.
 __device__ __forceinline__ uint32_t kth_legal(uint32_t k, const Legal& r, const WaveLds& L, int lane)
 {
     if (k >= r.total) return (uint32_t)PASS;
+    if (r.nl <= (uint32_t)LIST_CAP) {
+        const uint32_t d = (uint32_t)lane < r.nl ? L.lst[lane] : 0u;
+        const uint32_t w = (uint32_t)lane < r.nl ? L.mask[MASK_PAD + d] : 0u;
+        const uint32_t pc = (uint32_t)__popc(w);
+        uint32_t inc = pc;
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+            if (lane >= o) inc += y;
+        }
+        const int j = __builtin_ctzll(__ballot(inc > k));
+        const uint32_t kk = k - (rl(inc, j) - rl(pc, j));
+        return rl(d, j) * 32u + kth_bit(rl(w, j), kk, lane);
+    }
     uint32_t pc = 0;
     if (lane < KTH_LANES) {
         const uint4* w = (const uint4*)(L.mask + MASK_PAD) + lane * (KTH_WORDS / 4);
@@ -481,10 +496,8 @@ __device__ __forceinline__ uint32_t kth_legal(uint32_t k, const Legal& r, const 
         if (lane >= o) inc2 += y;
     }
     const int q = __builtin_ctzll(__ballot(lane < KTH_WORDS && inc2 > k));
-    uint32_t word = rl(w, q);
-    uint32_t kk = k - (rl(inc2, q) - rl(p2, q));
-    while (kk--) word &= word - 1;
-    return (uint32_t)(j * KTH_WORDS + q) * 32u + (uint32_t)__builtin_ctz(word);
+    const uint32_t kk = k - (rl(inc2, q) - rl(p2, q));
+    return (uint32_t)(j * KTH_WORDS + q) * 32u + kth_bit(rl(w, q), kk, lane);
 }
 
 // ---- obs -------------------------------------------------------------------------------------------------------
@@ -546,30 +559,6 @@ __device__ __forceinline__ uint4 expand_bits16(uint32_t x)   // 16 bits -> 16 by
 
 // (default-policy stores: nontemporal ones, a win for the lane-per-env games' full-line spans, measured 4.8 -> 6.0 ms
 // per launch here, where every row boundary splits a line between two waves)
-// bytes [lo, hi) of an aligned 16-B chunk, lo == 0 or hi == 16 (a row's first or last chunk): at most four
-// naturally aligned stores of 8 / 4 / 2 / 1 bytes instead of 16 predicated byte stores
-__device__ __forceinline__ void store_part(uint8_t* dst, int lo, int hi, const uint4& v)
-{
-    const uint64_t q0 = v.x | ((uint64_t)v.y << 32), q1 = v.z | ((uint64_t)v.w << 32);
-    if (lo == 0 && hi == 16) {
-        *(uint4*)dst = v;
-    } else if (lo == 0) {                // prefix [0, hi)
-        int p = 0;
-        uint64_t r = q0;
-        if (hi & 8) { *(uint64_t*)dst = q0; p = 8; r = q1; }
-        if (hi & 4) { *(uint32_t*)(dst + p) = (uint32_t)r; p += 4; r >>= 32; }
-        if (hi & 2) { *(uint16_t*)(dst + p) = (uint16_t)r; p += 2; r >>= 16; }
-        if (hi & 1) dst[p] = (uint8_t)r;
-    } else {                             // suffix [lo, 16): its bytes just below p sit at the top of r
-        const int len = 16 - lo;
-        int p = 16;
-        uint64_t r = q1;
-        if (len & 8) { *(uint64_t*)(dst + 8) = q1; p = 8; r = q0; }
-        if (len & 4) { p -= 4; *(uint32_t*)(dst + p) = (uint32_t)(r >> 32); r <<= 32; }
-        if (len & 2) { p -= 2; *(uint16_t*)(dst + p) = (uint16_t)(r >> 48); r <<= 16; }
-        if (len & 1) { p -= 1; dst[p] = (uint8_t)(r >> 56); }
-    }
-}
 
 // chunk q of a row misaligned by mis (its first byte is row byte 16 q - mis; bytes before the row are don't-care)
 __device__ __forceinline__ uint4 obs_chunk(const WaveLds& L, int q, int mis)
@@ -602,15 +591,19 @@ __device__ __forceinline__ void write_rows(const WaveLds& L, uint8_t* orow, uint
             if (q >= 1 && q < nchunks - 1) *(uint4*)(lrow - mis + 16 * q) = legal_chunk(L, q, mis);
         }
     }
-    // lanes 0 / 1: the obs row's first / last chunk, lanes 2 / 3: the legal row's
-    const bool is_obs = lane < 2;
+    // the two end chunks of both rows, one byte per lane in one store: lanes 0..15 / 16..31 the obs row's first / last
+    // chunk, 32..47 / 48..63 the legal row's
+    const bool is_obs = lane < 32;
     uint8_t* row = is_obs ? orow : lrow;
-    if (lane < 4 && row) {
+    if (row) {
         const int nbytes = is_obs ? OBS : LB;
         const int mis = (int)((uintptr_t)row & 15u), nchunks = (mis + nbytes + 15) >> 4;
-        const int q = (lane & 1) ? nchunks - 1 : 0, o = 16 * q - mis;
-        const uint4 v = is_obs ? obs_chunk(L, q, mis) : legal_chunk(L, q, mis);
-        store_part(row - mis + 16 * q, o < 0 ? -o : 0, nbytes - o < 16 ? nbytes - o : 16, v);
+        const int q = (lane & 16) ? nchunks - 1 : 0, o = 16 * q - mis + (lane & 15);   // row byte
+        if (o >= 0 && o < nbytes) {
+            const uint32_t x = 16u + (uint32_t)o;   // obs: bit of L.bv; legal: byte of L.mask (MASK_PAD = 4)
+            const uint32_t v = is_obs ? (L.bv[x >> 5] >> (x & 31u)) & 1u : ((const uint8_t*)L.mask)[x];
+            row[o] = (uint8_t)v;
+        }
     }
 }
 

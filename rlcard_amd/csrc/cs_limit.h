@@ -234,14 +234,14 @@ __device__ __forceinline__ bool deal9_swar(Rng& rng, uint32_t (&j)[9])
     if (k0 >= rng.sn || rng.sn - k0 < 28u) return false;
     const uint32_t* row = (const uint32_t*)(rng.stg + (k0 & ~3u));
     const uint32_t sh = k0 & 3u;
-    uint32_t w[7], x[6];
+    uint32_t w[7];
 #pragma unroll
     for (int q = 0; q < 7; q++) w[q] = row[q];
     uint32_t acc = 0, may = 0;
 #pragma unroll
     for (int q = 0; q < 6; q++) {
-        x[q] = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh) & 0x3F3F3F3Fu;   // staged bytes k0 + 4q .., & 63
-        const uint32_t ge43 = (x[q] + 0x55555555u) & 0x80808080u, ge52 = (x[q] + 0x4C4C4C4Cu) & 0x80808080u;
+        const uint32_t x = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh) & 0x3F3F3F3Fu;   // bytes k0 + 4q .., & 63
+        const uint32_t ge43 = (x + 0x55555555u) & 0x80808080u, ge52 = (x + 0x4C4C4C4Cu) & 0x80808080u;
         const uint32_t a = (~ge43 & 0x80808080u) >> 7, m = (ge43 & ~ge52) >> 7;
         // byte flags (bits 0, 8, 16, 24) -> 4-bit mask: the product's top nibble
         acc |= ((a * 0x10204080u) >> 28) << (4 * q);
@@ -252,10 +252,7 @@ __device__ __forceinline__ bool deal9_swar(Rng& rng, uint32_t (&j)[9])
         may &= may - 1u;
         const uint32_t cnt = __popc(acc & ((1u << t) - 1u));
         if (cnt >= 9u) break;                    // past the ninth draw: not consumed
-        uint32_t d = x[0];
-#pragma unroll
-        for (int q = 1; q < 6; q++) d = (t >> 2) == (uint32_t)q ? x[q] : d;
-        const uint32_t u = (d >> (8u * (t & 3u))) & 63u;
+        const uint32_t u = rng.stg[k0 + t] & 63u;   // the staged byte again (LDS), not a select over x[]
         acc |= u <= 51u - cnt ? 1u << t : 0u;
     }
     if (__popc(acc) < 9) return false;
@@ -462,18 +459,20 @@ struct Limit {
         return m;
     }
 
+    // the cards as a 64-bit mask (ids < 52), the four raise one-hots as a 20-bit field at obs bit 52
     __device__ __forceinline__ void observe(int player, uint32_t (&bits)[NB]) const
     {
-        bits[0] = bits[1] = bits[2] = 0;
         const int r = rc(), npub = r == 0 ? 0 : (r == 1 ? 3 : (r == 2 ? 4 : 5));
+        uint64_t cm = 1ull << hole(player, 0) | 1ull << hole(player, 1);
 #pragma unroll
-        for (int k = 0; k < 5; k++)
-            if (k < npub) set_bit(bits, board(k));
-        set_bit(bits, hole(player, 0));
-        set_bit(bits, hole(player, 1));
+        for (int k = 0; k < 5; k++) cm |= (uint64_t)(k < npub) << board(k);
         const uint32_t rn = use_prev() ? (w3 >> 12) : w3;
+        uint32_t R = 0;
 #pragma unroll
-        for (int i = 0; i < 4; i++) set_bit(bits, 52 + 5 * i + (int)((rn >> (3 * i)) & 7u));
+        for (int i = 0; i < 4; i++) R |= 1u << (5 * i + (int)((rn >> (3 * i)) & 7u));
+        bits[0] = (uint32_t)cm;
+        bits[1] = (uint32_t)(cm >> 32) | R << 20;
+        bits[2] = R >> 12;
     }
 
     // the deal of init_game (game.py:46-95): shuffle + holes + board, then the small blind seat randint(0, 2)

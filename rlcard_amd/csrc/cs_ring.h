@@ -158,6 +158,12 @@ __device__ __forceinline__ void ring_st(gu32* p, uint32_t v)
     else *p = v;
 }
 
+// ring bytes of a refill: every lane stores its word's byte (one global_store_byte per 64 words) instead of packing
+// four lanes' bytes with DPP moves into a dword store by every fourth lane
+#ifndef CS_RING_BYTE_ST
+#define CS_RING_BYTE_ST 1
+#endif
+
 // Wave-cooperative refill of one env: blocks L+1..L+3 from wbuf (block L, slot lat). All 64 lanes must call.
 __device__ __forceinline__ void ring_gen_wave(gu32* wbuf, uint32_t lat, int lane, uint32_t phx = 0)
 {
@@ -179,12 +185,18 @@ __device__ __forceinline__ void ring_gen_wave(gu32* wbuf, uint32_t lat, int lane
         const uint32_t slot = (lat + (uint32_t)b) & SLOT_MASK;
 #pragma unroll
         for (int c = 0; c < 10; c++) {
-            const int t = (int)(mt_temper(n[c]) & 255u);
-            const uint32_t t1 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x101, 0xF, 0xF, true);  // row_shl:1
-            const uint32_t t2 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x102, 0xF, 0xF, true);  // row_shl:2
-            const uint32_t t3 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x103, 0xF, 0xF, true);  // row_shl:3
-            if ((lane & 3) == 0 && (c < 9 || lane < 48))
-                ring_st(ring + slot * (MT_N / 4) + 16 * c + (lane >> 2), (uint32_t)t | (t1 << 8) | (t2 << 16) | (t3 << 24));
+            if constexpr (CS_RING_BYTE_ST) {
+                if (c < 9 || lane < 48)
+                    ((gu8*)(ring + slot * (MT_N / 4)))[64 * c + lane] = (uint8_t)mt_temper(n[c]);
+            } else {
+                const int t = (int)(mt_temper(n[c]) & 255u);
+                const uint32_t t1 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x101, 0xF, 0xF, true);  // row_shl:1
+                const uint32_t t2 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x102, 0xF, 0xF, true);  // row_shl:2
+                const uint32_t t3 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x103, 0xF, 0xF, true);  // row_shl:3
+                if ((lane & 3) == 0 && (c < 9 || lane < 48))
+                    ring_st(ring + slot * (MT_N / 4) + 16 * c + (lane >> 2),
+                            (uint32_t)t | (t1 << 8) | (t2 << 16) | (t3 << 24));
+            }
             o[c] = n[c];
         }
     }

@@ -577,7 +577,9 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
         uint32_t bits[G::NB];
         g.observe(p, bits);
         const uint32_t pr = pol.at(seed, genv, t0 + (uint64_t)t, t == 0);
-        const int a = G::A <= 32 ? pick_legal32((uint32_t)lg, pr) : pick_legal(lg, pr);
+        int a;
+        if constexpr (G::A <= 8) a = pick_legal_small<G::A>((uint32_t)lg, pr);
+        else a = G::A <= 32 ? pick_legal32((uint32_t)lg, pr) : pick_legal(lg, pr);
 #ifndef CS_PROF_NO_OBS   // profiling builds only (tools: make variant DEFS=-DCS_PROF_NO_OBS): outputs incomplete
         emit_obs<G, G::EPW>(lds[c.wid], bits, obs, rowbase + c.wave_first, flags, c);
 #endif
