@@ -107,6 +107,7 @@ std::string table_build_host(std::vector<uint8_t>& host, size_t off[4], Tab* tab
     tab->bomb_lo = type_lo[TYPE_BOMB];
     tab->bomb_hi = type_hi[TYPE_BOMB];
     tab->rocket = type_lo[TYPE_ROCKET];
+    for (int k = 0; k <= MAX_GROUPS / 32; k++) tab->kfirst[k] = 32 * k < ng ? gstart[32 * k] : PASS;
     return "";
 }
 

@@ -46,6 +46,9 @@ struct Tab {
     const uint32_t* drange;  // [ND]
     int32_t ng;
     int32_t bomb_lo, bomb_hi, rocket;
+    // kfirst[k]: the first id of group 32 k (PASS past the last group): the ids of groups 32 k .. 32 k + 31 lie in
+    // [kfirst[k], kfirst[k + 1]), so a 32-group pass of the legal scan that no candidate range meets is skipped
+    int32_t kfirst[MAX_GROUPS / 32 + 1];
 };
 
 // Packed env state (u32 words, env-major: st[env * WORDS + w]):

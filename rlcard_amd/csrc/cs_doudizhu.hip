@@ -164,8 +164,12 @@ struct Env {
     // Player.play + Round.proceed_round + Game.step (player.py:88-108, round.py:54-79, game.py:55-81)
     __device__ __forceinline__ void apply(uint32_t a, const Tab& tb, int lane)
     {
+        apply_with(a, a != (uint32_t)PASS ? tb.cnt[a] : 0ull, a != (uint32_t)PASS ? (uint32_t)tb.gid[a] : 0u, lane);
+    }
+    // the same with the action's table entries (packed counts, group) already loaded
+    __device__ __forceinline__ void apply_with(uint32_t a, uint64_t c, uint32_t gid, int lane)
+    {
         const uint32_t p = cur;
-        const uint64_t c = a != (uint32_t)PASS ? tb.cnt[a] : 0ull;
         const uint64_t down = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)hcnt, 1) |
                               ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(hcnt >> 32), 1) << 32);
         hcnt = lane == 11 ? c : (lane >= 3 && lane < 11 ? down : 0ull);
@@ -176,7 +180,7 @@ struct Env {
         hw4 = a | (NO_ACTION << 16);
         ntrace++;
         if (a != (uint32_t)PASS) {
-            ggrp = tb.gid[a];
+            ggrp = gid;
             const uint64_t c0 = keep64(p == 0, c), c1 = keep64(p == 1, c), c2 = keep64(p == 2, c);
             h0 -= c0; h1 -= c1; h2 -= c2;
             q0 += c0; q1 += c1; q2 += c2;
@@ -197,6 +201,12 @@ struct Cand {
     __device__ __forceinline__ bool ok(uint32_t x) const
     {
         return (x - c_lo < c_len) | (x - b_lo < b_len) | (x - r_lo < r_len);
+    }
+    // does any candidate range meet the ids [lo, hi)?
+    __device__ __forceinline__ bool meets(uint32_t lo, uint32_t hi) const
+    {
+        return (c_len && c_lo < hi && c_lo + c_len > lo) | (b_len && b_lo < hi && b_lo + b_len > lo) |
+               (r_len && r_lo < hi && r_lo + r_len > lo);
     }
 };
 __device__ __forceinline__ Cand cand_of(const Env& e, const Tab& tb, const TabLds& T)
@@ -561,16 +571,16 @@ __device__ __forceinline__ uint4 expand_bits16(uint32_t x)   // 16 bits -> 16 by
 // per launch here, where every row boundary splits a line between two waves)
 
 // chunk q of a row misaligned by mis (its first byte is row byte 16 q - mis; bytes before the row are don't-care)
-__device__ __forceinline__ uint4 obs_chunk(const WaveLds& L, int q, int mis)
+__device__ __forceinline__ uint4 obs_chunk(const uint32_t* bv, int q, int mis)
 {
-    const int bp = 16 * q - mis + 16;                               // bit of L.bv, >= 1
-    const uint64_t two = (uint64_t)L.bv[bp >> 5] | ((uint64_t)L.bv[(bp >> 5) + 1] << 32);
+    const int bp = 16 * q - mis + 16;                               // bit of bv, >= 1
+    const uint64_t two = (uint64_t)bv[bp >> 5] | ((uint64_t)bv[(bp >> 5) + 1] << 32);
     return expand_bits16((uint32_t)(two >> (bp & 31)) & 0xFFFFu);
 }
-__device__ __forceinline__ uint4 legal_chunk(const WaveLds& L, int q, int mis)
+__device__ __forceinline__ uint4 legal_chunk(const uint32_t* mask, int q, int mis)
 {
-    const int sb = 4 * MASK_PAD + 16 * q - mis;                     // byte of L.mask, >= 1
-    const uint32_t* w = L.mask + (sb >> 2);
+    const int sb = 4 * MASK_PAD + 16 * q - mis;                     // byte of the mask image, >= 1
+    const uint32_t* w = mask + (sb >> 2);
     const int sh = sb & 3;                                          // alignbyte(x, y, 0) = y
     return make_uint4(__builtin_amdgcn_alignbyte(w[1], w[0], sh), __builtin_amdgcn_alignbyte(w[2], w[1], sh),
                       __builtin_amdgcn_alignbyte(w[3], w[2], sh), __builtin_amdgcn_alignbyte(w[4], w[3], sh));
@@ -581,14 +591,14 @@ __device__ __forceinline__ void write_rows(const WaveLds& L, uint8_t* orow, uint
 {
     if (orow) {
         const int mis = (int)((uintptr_t)orow & 15u), nchunks = (mis + OBS + 15) >> 4;   // <= 58
-        if (lane >= 1 && lane < nchunks - 1) *(uint4*)(orow - mis + 16 * lane) = obs_chunk(L, lane, mis);
+        if (lane >= 1 && lane < nchunks - 1) *(uint4*)(orow - mis + 16 * lane) = obs_chunk(L.bv, lane, mis);
     }
     if (lrow) {
         const int mis = (int)((uintptr_t)lrow & 15u), nchunks = (mis + LB + 15) >> 4;    // <= 216
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int q = j * WAVE + lane;
-            if (q >= 1 && q < nchunks - 1) *(uint4*)(lrow - mis + 16 * q) = legal_chunk(L, q, mis);
+            if (q >= 1 && q < nchunks - 1) *(uint4*)(lrow - mis + 16 * q) = legal_chunk(L.mask, q, mis);
         }
     }
     // the two end chunks of both rows, one byte per lane in one store: lanes 0..15 / 16..31 the obs row's first / last
@@ -813,6 +823,483 @@ __global__ __launch_bounds__(BLOCK, CS_DDZ_MINW) void k_rollout(uint32_t* mt, ui
     if (lane == 0) m.save(ctl, c.env);
 }
 
+// ---- the rollout with TWO envs per wave ---------------------------------------------------------------------------
+// Lanes 0..31 play one env and lanes 32..63 the next: every step below runs for both envs in the same instructions
+// (each half-wave is one env's 32 lanes), so the game logic that the one-env kernels run as wave-uniform scalar code
+// -- the scalar unit is their busiest pipe -- becomes vector code shared by two envs, and the two envs' dependency
+// chains (LDS round trips, table loads) overlap inside one wave. Same functions of the same state, same outputs:
+// the per-env values are simply held per lane (uniform within a half). The deal (rare: once per game) still runs with
+// the whole wave for one env at a time, through the one-env `deal`.
+#ifndef CS_DDZ_PAIR
+#define CS_DDZ_PAIR 1
+#endif
+#ifndef CS_DDZ_PAIR_WAVES
+#define CS_DDZ_PAIR_WAVES 8   // waves per block: the group table in LDS is shared by 16 envs
+#endif
+#ifndef CS_DDZ_LROW_UNROLL
+#define CS_DDZ_LROW_UNROLL 4  // legal-row chunk loads in flight (unrolled iterations of 32 lanes per env)
+#endif
+#ifndef CS_DDZ_PAIR_MINW
+#define CS_DDZ_PAIR_MINW 4    // waves per SIMD the registers must allow (LDS allows 4: two 79-KB blocks per CU)
+#endif
+constexpr int HW = WAVE / 2;                         // lanes per env
+constexpr int PWPB = CS_DDZ_PAIR_WAVES, PBLOCK = PWPB * WAVE;
+constexpr int NCH = (ND + HW - 1) / HW;              // 27 chunks of 32 mask dwords
+// The pair kernel keeps the legal mask image SHIFTED by the legal row's misalignment mis (row byte o at image byte
+// 16 + mis + o), so the row's 16-B chunks are aligned 16-B blocks of the image (ds_read_b128, no bank conflicts, no
+// byte alignment); a mask dword is written / read at byte 16 + mis + 4 d (2-byte aligned: mis is even).
+struct alignas(16) PairLds {
+    uint32_t mask[MASK_WORDS];                       // the shifted image (see above)
+    union {
+        uint16_t pre[MAX_GROUPS + 8];                // the legal scan's group prefix counts, dead once it is done:
+        struct {                                     // the obs image reuses the space
+            uint64_t segv[NSEG];
+            uint32_t bv[BV_WORDS];
+        } o;
+    } u;
+    uint16_t lst[LIST_RING];
+};
+static_assert(MAX_GROUPS % HW == 0 && NSEG <= HW && BV_WORDS == HW && NCH <= HW, "pair layout");
+
+__device__ __forceinline__ uint32_t half32(uint64_t b, int lane) { return lane < HW ? (uint32_t)b : (uint32_t)(b >> 32); }
+__device__ __forceinline__ uint32_t below32(uint32_t m, int hl) { return (uint32_t)__popc(m & ((1u << hl) - 1u)); }
+// v at lane k of this lane's half (k may differ per lane)
+__device__ __forceinline__ uint32_t hshfl(uint32_t v, int lane, uint32_t k)
+{
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((uint32_t)(lane & HW) + (k & (HW - 1))) << 2), (int)v);
+}
+__device__ __forceinline__ uint64_t hshfl64(uint64_t v, int lane, uint32_t k)
+{
+    return (uint64_t)hshfl((uint32_t)v, lane, k) | ((uint64_t)hshfl((uint32_t)(v >> 32), lane, k) << 32);
+}
+
+// mask dword d of the shifted image (byte 16 + mis + 4 d: mis even, so 4- or 2-byte aligned)
+__device__ __forceinline__ void put_mask(PairLds& L, uint32_t d, uint32_t mis, uint32_t v)
+{
+    const uint32_t b = 16u + mis + 4u * d;
+    if ((b & 3u) == 0u) {
+        L.mask[b >> 2] = v;
+    } else {
+        uint16_t* h = (uint16_t*)L.mask + (b >> 1);
+        h[0] = (uint16_t)v;
+        h[1] = (uint16_t)(v >> 16);
+    }
+}
+__device__ __forceinline__ uint32_t get_mask(const PairLds& L, uint32_t d, uint32_t mis)
+{
+    const uint32_t b = 16u + mis + 4u * d;
+    return __builtin_amdgcn_alignbyte(L.mask[(b >> 2) + 1], L.mask[b >> 2], b & 3u);
+}
+
+// pass c (see build_legal) for the listed dwords [t0, lim) of each half's env, up to 4 per env
+__device__ __forceinline__ void test_listed2(uint32_t t0, uint32_t lim, uint64_t h, const Cand& c, const Tab& tb,
+                                             PairLds& L, uint32_t mis, int lane, Legal& r)
+{
+    const int hl = lane & (HW - 1);
+    uint64_t cnt[4];
+    uint32_t id[4], dw[4];
+    bool live[4], ent[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t e = t0 + (uint32_t)q;
+        ent[q] = e < lim;
+        dw[q] = ent[q] ? L.lst[e & (LIST_RING - 1)] : 0u;
+        id[q] = dw[q] * 32u + (uint32_t)hl;
+        live[q] = ent[q] && id[q] < (uint32_t)PASS;
+        cnt[q] = live[q] ? tb.cnt[id[q]] : ~0ull;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t m = half32(__ballot(live[q] && contains(h, cnt[q]) && c.ok(id[q])), lane);
+        if (hl == 0 && ent[q]) put_mask(L, dw[q], mis, m);
+        r.total += (uint32_t)__popc(m);
+    }
+}
+
+// build_legal for each half's env (act: the half holds a live env); the mask image must be zero on entry
+__device__ __forceinline__ Legal build_legal2(const Env& e, const Cand& c, const Tab& tb, const TabLds& T, PairLds& L,
+                                              uint32_t mis, int lane, bool act)
+{
+    const int hl = lane & (HW - 1);
+    Legal r;
+    r.total = 0;
+    r.nl = 0;
+    act = act && !e.over();
+    const uint64_t h = e.hand(e.cur);
+    // a. groups, 32 per pass and env; a pass whose groups no candidate range of either env meets only writes the
+    // prefix counts (following a play: the same type's greater weights, the bombs, the rocket)
+    uint32_t base = 0;
+#pragma unroll
+    for (int k = 0; k < MAX_GROUPS / HW; k++) {
+        const int g = k * HW + hl;
+        const bool may = act && c.meets((uint32_t)tb.kfirst[k], (uint32_t)tb.kfirst[k + 1]);
+        if (__ballot(may)) {
+            bool pass = false;
+            if (may && g < tb.ng) {
+                const uint4 q = T.grp[g];
+                pass = contains(h, (uint64_t)q.x | ((uint64_t)q.y << 32)) && c.ok(q.z & 0xFFFFu);
+            }
+            const uint32_t m = half32(__ballot(pass), lane);
+            if (g <= tb.ng) L.u.pre[g] = (uint16_t)(base + below32(m, hl));
+            base += (uint32_t)__popc(m);
+        } else if (g <= tb.ng) {
+            L.u.pre[g] = (uint16_t)base;
+        }
+    }
+    act = act && base != 0;
+    if (!__ballot(act)) return r;
+    wave_sync_lds();
+    // b. chunks of 32 dwords that any passing group reaches (lane k of a half: chunk k), their dwords listed in order;
+    // c. 4 listed dwords per env and batch
+    bool chp = false;
+    if (act && hl < NCH) {
+        const int last = hl * HW + HW - 1 < ND ? hl * HW + HW - 1 : ND - 1;
+        const uint32_t lo = T.drange[hl * HW] & 0xFFFFu, hi = T.drange[last] >> 16;
+        chp = L.u.pre[hi + 1] > L.u.pre[lo];
+    }
+    uint32_t chunks = half32(__ballot(chp), lane);
+    uint32_t tested = 0;
+    while (__ballot(chunks != 0u)) {
+        const bool has = chunks != 0u;
+        const int k = has ? __builtin_ctz(chunks) : 0;
+        chunks &= chunks - 1u;
+        const int d = k * HW + hl;
+        bool pass = false;
+        if (has && d < ND) {
+            const uint32_t dr = T.drange[d];
+            pass = L.u.pre[(dr >> 16) + 1] > L.u.pre[dr & 0xFFFFu];
+        }
+        const uint32_t m = half32(__ballot(pass), lane);
+        if (pass) L.lst[(r.nl + below32(m, hl)) & (LIST_RING - 1)] = (uint16_t)d;
+        r.nl += (uint32_t)__popc(m);
+        while (__ballot(r.nl - tested >= 4u)) {
+            const bool full = r.nl - tested >= 4u;
+            test_listed2(tested, full ? tested + 4u : tested, h, c, tb, L, mis, lane, r);
+            tested += full ? 4u : 0u;
+        }
+    }
+    if (__ballot(tested < r.nl)) test_listed2(tested, r.nl, h, c, tb, L, mis, lane, r);
+    return r;
+}
+
+// kth_legal's two-level scan over one env's whole mask image, all 64 lanes (k < the env's legal combos); the image's
+// bits are in id order, shifted by 8 mis bits: the result is the k-th set bit's position from byte 16, minus 8 mis
+__device__ __forceinline__ uint32_t kth_full(uint32_t k, const uint32_t* mask, int lane)
+{
+    uint32_t pc = 0;
+    if (lane < KTH_LANES) {
+        const uint4* w = (const uint4*)(mask + MASK_PAD) + lane * (KTH_WORDS / 4);
+#pragma unroll
+        for (int j = 0; j < KTH_WORDS / 4; j++) {
+            const uint4 x = w[j];
+            pc += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+        }
+    }
+    uint32_t inc = pc;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+        if (lane >= o) inc += y;
+    }
+    const int j = __builtin_ctzll(__ballot(inc > k));
+    k -= rl(inc, j) - rl(pc, j);
+    const uint32_t w = lane < KTH_WORDS ? mask[MASK_PAD + j * KTH_WORDS + lane] : 0u;
+    const uint32_t p2 = (uint32_t)__popc(w);
+    uint32_t inc2 = p2;
+#pragma unroll
+    for (int o = 1; o < KTH_WORDS; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc2, o);
+        if (lane >= o) inc2 += y;
+    }
+    const int q = __builtin_ctzll(__ballot(lane < KTH_WORDS && inc2 > k));
+    const uint32_t kk = k - (rl(inc2, q) - rl(p2, q));
+    return (uint32_t)(j * KTH_WORDS + q) * 32u + kth_bit(rl(w, q), kk, lane);
+}
+
+// kth_legal for each half's env: the listed dwords (at most 32: one per lane of the half), else the env's full scan
+__device__ __forceinline__ uint32_t kth_legal2(uint32_t k, const Legal& r, PairLds (&PL)[2], uint32_t mis, int lane)
+{
+    const int hl = lane & (HW - 1), hf = lane >> 5;
+    const PairLds& L = PL[hf];
+    const bool pick = k < r.total;
+    const bool fast = pick && r.nl <= (uint32_t)HW, slow = pick && r.nl > (uint32_t)HW;
+    uint32_t res = (uint32_t)PASS;
+    if (__ballot(fast)) {
+        const bool in = fast && (uint32_t)hl < r.nl;
+        const uint32_t d = in ? L.lst[hl] : 0u;
+        const uint32_t w = in ? get_mask(L, d, mis) : 0u;
+        const uint32_t pc = (uint32_t)__popc(w);
+        uint32_t inc = pc;
+#pragma unroll
+        for (int o = 1; o < HW; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)inc, o, HW);
+            if (hl >= o) inc += y;
+        }
+        const uint32_t jm = half32(__ballot(inc > k), lane);
+        const uint32_t j = jm ? (uint32_t)__builtin_ctz(jm) : 0u;
+        const uint32_t incj = hshfl(inc, lane, j), pcj = hshfl(pc, lane, j), wj = hshfl(w, lane, j), dj = hshfl(d, lane, j);
+        const uint32_t kk = k - (incj - pcj);
+        const uint32_t bm = half32(__ballot(((wj >> hl) & 1u) && below32(wj, hl) == kk), lane);
+        if (fast) res = dj * 32u + (bm ? (uint32_t)__builtin_ctz(bm) : 0u);
+    }
+    const uint64_t sb = __ballot(slow);
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        if ((sb >> (HW * j)) & 1u) {
+            const uint32_t id = kth_full(rl(k, HW * j), PL[j].mask, lane) - 8u * rl(mis, HW * j);
+            if (slow && hf == j) res = id;
+        }
+    }
+    return res;
+}
+
+// build_obs for each half's env, observed by `self` (per half)
+__device__ __forceinline__ void build_obs2(const Env& e, uint32_t self, PairLds& L, int lane)
+{
+    const int hl = lane & (HW - 1);
+    const uint32_t nt = e.ntrace;
+    const uint32_t h8 = e.hw4 & 0xFFFFu;
+    const uint32_t mate = 3u - self;
+    const uint64_t last_c = hshfl64(e.hcnt, lane, h8 == (uint32_t)PASS ? 10u : 11u);   // last non-pass action
+    const uint64_t llv = hshfl64(e.hcnt, lane, 11u - (nt - 1u) % 3u);                 // landlord's last action
+    const uint64_t ltv = hshfl64(e.hcnt, lane, 11u - (nt - 1u - mate) % 3u);          // teammate's last action
+    const uint64_t ll_c = (self != 0u && nt >= 1u) ? llv : 0ull, lt_c = (self != 0u && nt > mate) ? ltv : 0ull;
+    const int s = hl;
+    const uint64_t u1 = e.hand(self == 0 ? 1u : 0u) + e.hand(self == 2 ? 1u : 2u);
+    const uint64_t u12 = self == 0 ? e.q2 : e.q0, u13 = self == 0 ? e.q1 : e.played(mate);
+    const uint64_t direct = keep64(s == 0, e.hand(self)) | keep64(s == 1, u1) | keep64(s == 2, last_c) |
+                            keep64(s >= 3 && s <= 11, e.hcnt) | keep64(s == 12, u12) | keep64(s == 13, u13) |
+                            keep64(s == 14, ll_c) | keep64(s == 15, lt_c);
+    if (s < NSEG) L.u.o.segv[s] = cards_bits(direct);
+    uint32_t p1, p2;
+    if (self == 0) {
+        const uint32_t n2 = num_cards(e.h2), n1 = num_cards(e.h1);
+        p1 = 756u + (n2 >= 1u ? n2 - 1u : 16u);
+        p2 = 773u + (n1 >= 1u ? n1 - 1u : 16u);
+    } else {
+        const uint32_t n0 = num_cards(e.h0), nm = num_cards(e.hand(mate));
+        p1 = 864u + (n0 >= 1u ? n0 - 1u : 19u);
+        p2 = 884u + (nm >= 1u ? nm - 1u : 16u);
+    }
+    wave_sync_lds();
+    const int x0 = hl == 0 ? 0 : 32 * hl - 16;
+    const int sg = x0 / 54, off = x0 - 54 * sg;
+    const uint32_t v = (uint32_t)((L.u.o.segv[sg] >> off) | (L.u.o.segv[sg + 1] << (54 - off)));
+    const uint32_t d1 = p1 - (uint32_t)x0, d2 = p2 - (uint32_t)x0;
+    L.u.o.bv[hl] = hl == 0 ? v << 16 : v | keep32(d1 < 32u, 1u << (d1 & 31u)) | keep32(d2 < 32u, 1u << (d2 & 31u));
+}
+
+// write_rows for each half's env
+__device__ __forceinline__ void write_rows2(const PairLds& L, uint8_t* orow, uint8_t* lrow, int lane)
+{
+    const int hl = lane & (HW - 1);
+    if (orow) {
+        const int mis = (int)((uintptr_t)orow & 15u), nchunks = (mis + OBS + 15) >> 4;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int q = j * HW + hl;
+            if (q >= 1 && q < nchunks - 1) *(uint4*)(orow - mis + 16 * q) = obs_chunk(L.u.o.bv, q, mis);
+        }
+    }
+    if (lrow) {   // chunk q = image block q + 1 (the image is shifted by the row's misalignment)
+        const int mis = (int)((uintptr_t)lrow & 15u), nchunks = (mis + LB + 15) >> 4;
+#pragma unroll CS_DDZ_LROW_UNROLL
+        for (int j = 0; j < (216 + HW - 1) / HW; j++) {
+            const int q = j * HW + hl;
+            if (q >= 1 && q < nchunks - 1) *(uint4*)(lrow - mis + 16 * q) = ((const uint4*)L.mask)[q + 1];
+        }
+    }
+    // the rows' end chunks, a byte per lane: lanes 0..15 / 16..31 of a half the first / last chunk
+#pragma unroll
+    for (int rr = 0; rr < 2; rr++) {
+        uint8_t* row = rr ? lrow : orow;
+        if (row) {
+            const int nbytes = rr ? LB : OBS;
+            const int mis = (int)((uintptr_t)row & 15u), nchunks = (mis + nbytes + 15) >> 4;
+            const int q = (hl & 16) ? nchunks - 1 : 0, o = 16 * q - mis + (hl & 15);
+            if (o >= 0 && o < nbytes) {
+                const uint32_t x = 16u + (uint32_t)o;
+                row[o] = (uint8_t)(rr ? ((const uint8_t*)L.mask)[x + (uint32_t)mis] : (L.u.o.bv[x >> 5] >> (x & 31u)) & 1u);
+            }
+        }
+    }
+}
+
+// the stream position of each half's env (WaveMt fields per lane)
+struct PairMt {
+    uint32_t pos, stale, dabs;
+    uint64_t key;
+};
+
+// deal a new game to half j's env with the whole wave (the one-env `deal`), then hand it to the half
+template <bool PHX>
+__device__ __forceinline__ void deal_half(int j, Env& e, uint32_t& dlo, uint32_t& dhi, PairMt& pm, uint32_t* mt,
+                                          int64_t env_h, int lane)
+{
+    const int src = HW * j;
+    WaveMt<PHX> m;
+    const int64_t ej = (int64_t)rl((uint32_t)env_h, src) | ((int64_t)rl((uint32_t)((uint64_t)env_h >> 32), src) << 32);
+    m.base = mt + ej * MT_WORDS;
+    m.pos = rl(pm.pos, src);
+    m.stale = rl(pm.stale, src);
+    m.dabs = rl(pm.dabs, src);
+    m.key = rl64(pm.key, src);
+    Env es;
+    deal(es, m, lane);
+    const uint32_t lo = (uint32_t)__shfl((int)es.deck, lane & (HW - 1)), hi = (uint32_t)__shfl((int)es.deck, HW + (lane & (HW - 1)));
+    if ((lane >> 5) == j) {
+        e = es;
+        dlo = lo;
+        dhi = (lane & (HW - 1)) < 54 - HW ? hi : 0u;
+        pm.pos = m.pos;
+        pm.stale = m.stale;
+        pm.dabs = m.dabs;
+    }
+}
+
+template <bool PHX>
+__global__ __launch_bounds__(PBLOCK, CS_DDZ_PAIR_MINW) void k_rollout2(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n, int T,
+                                                     uint64_t seed, uint64_t t0, uint64_t env_base, cs_traj_out out,
+                                                     Tab tb)
+{
+    __shared__ PairLds lds[PWPB][2];
+    __shared__ TabLds tl;
+    load_tab(tl, tb);                 // every thread of the block, before any wave leaves
+    const int lane = (int)(threadIdx.x & (WAVE - 1)), hl = lane & (HW - 1), hf = lane >> 5;
+    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+    const int64_t env = (int64_t)blockIdx.x * (2 * PWPB) + 2 * wid + hf;
+    const bool valid = env < n;
+    if (!__ballot(valid)) return;
+    PairLds (&PL)[2] = lds[wid];
+    PairLds& L = PL[hf];
+    // the env's state words (lanes 0..31 of its half: words 0..31, lanes 0..3: 32..35) and stream position
+    const uint32_t* srow = st + (valid ? env : 0) * WORDS;
+    const uint32_t wlo = valid ? srow[hl] : 0u, whi = valid && hl < WORDS - HW ? srow[HW + hl] : 0u;
+    auto F = [&](uint32_t w) { return hshfl(wlo, lane, w); };
+    Env e;
+    e.h0 = (uint64_t)F(0) | ((uint64_t)F(1) << 32);
+    e.h1 = (uint64_t)F(2) | ((uint64_t)F(3) << 32);
+    e.h2 = (uint64_t)F(4) | ((uint64_t)F(5) << 32);
+    e.q0 = (uint64_t)F(6) | ((uint64_t)F(7) << 32);
+    e.q1 = (uint64_t)F(8) | ((uint64_t)F(9) << 32);
+    e.q2 = (uint64_t)F(10) | ((uint64_t)F(11) << 32);
+    e.hw0 = F(W_HIST);
+    e.hw1 = F(W_HIST + 1);
+    e.hw2 = F(W_HIST + 2);
+    e.hw3 = F(W_HIST + 3);
+    const uint32_t w16 = F(W_HIST + 4);
+    e.hw4 = w16 | (NO_ACTION << 16);
+    e.ggrp = w16 >> 16;
+    {
+        const uint32_t id = hl >= 3 && hl <= 11 ? e.hist((uint32_t)(hl - 3)) : NO_ACTION;
+        e.hcnt = id < (uint32_t)PASS ? tb.cnt[id] : 0ull;
+    }
+    e.ntrace = F(W_NTRACE);
+    {
+        const uint32_t g = F(W_GREATER), c = F(W_CUR);
+        e.greater = g & 0xFFFFu;
+        e.gplay = g >> 16;
+        e.cur = c & 0xFFu;
+        e.winner = valid ? (c >> 8) & 0xFFu : 0u;   // a missing env stays "over" and is never dealt
+    }
+    (void)whi;
+    e.deck = 0;
+    const uint8_t* dk = (const uint8_t*)(srow + W_DECK);
+    uint32_t dlo = valid ? dk[hl] : 0u, dhi = valid && hl < 54 - HW ? dk[HW + hl] : 0u;
+    PairMt pm;
+    {
+        const uint32_t w = valid ? ctl[env] : 0u;
+        pm.pos = w & 0x7FFu;
+        pm.stale = (w >> 16) & 1u;
+        pm.dabs = 0;
+        pm.key = 0;
+        if constexpr (PHX) {
+            const uint32_t* b = mt + (valid ? env : 0) * MT_WORDS;
+            pm.key = valid ? (uint64_t)b[0] | (uint64_t)b[1] << 32 : 0ull;
+            pm.dabs = valid ? b[2] : 0u;
+        }
+    }
+    {
+        const uint64_t need = __ballot(valid && e.over());
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+            if ((need >> (HW * j)) & 1u) deal_half<PHX>(j, e, dlo, dhi, pm, mt, env, lane);
+    }
+    const uint64_t genv = env_base + (uint64_t)env;
+    uint32_t rr_lane = 0;
+    for (int t = 0; t < T; t++) {
+        const int64_t row = (int64_t)t * n + env;
+        {   // zero the mask image of both envs: 218 uint4 each, 32 lanes per env
+            uint4* z = (uint4*)L.mask;
+#pragma unroll
+            for (int j = 0; j < (MASK_WORDS / 4 + HW - 1) / HW; j++) {
+                const int q = j * HW + hl;
+                if (q < MASK_WORDS / 4) z[q] = make_uint4(0, 0, 0, 0);
+            }
+        }
+        wave_sync_lds();
+        const uint32_t lmis = (uint32_t)(((uintptr_t)out.legal + (uint64_t)row * LB) & 15u);   // the image's shift
+        const Cand cd = cand_of(e, tb, tl);
+        const Legal lg = build_legal2(e, cd, tb, tl, L, lmis, lane, valid);
+        build_obs2(e, e.cur, L, lane);
+        wave_sync_lds();
+        const uint32_t count = lg.total + (cd.leading ? 0u : 1u);
+        if ((t & (HW - 1)) == 0) rr_lane = philox_u32(seed, genv, t0 + (uint64_t)(t + hl));
+        const uint32_t rr = hshfl(rr_lane, lane, (uint32_t)(t & (HW - 1)));
+        const uint32_t a = kth_legal2((uint32_t)(((uint64_t)rr * count) >> 32), lg, PL, lmis, lane);
+        // the action's table entries, loaded now so that their latency hides behind the row writes
+        const bool play = valid && a != (uint32_t)PASS;
+        const uint64_t ca = play ? tb.cnt[a] : 0ull;
+        const uint32_t ga = play ? (uint32_t)tb.gid[a] : 0u;
+        if (valid && !cd.leading && hl == 0) ((uint8_t*)L.mask)[16u + lmis + PASS / 8] |= (uint8_t)(1u << (PASS & 7));
+        wave_sync_lds();
+        write_rows2(L, valid && !(CS_PROF_DDZ & 2) ? (uint8_t*)out.obs + row * OBS : nullptr,
+                    valid && !(CS_PROF_DDZ & 1) ? (uint8_t*)out.legal + row * LB : nullptr, lane);
+        const uint32_t p = e.cur;
+        if (valid) e.apply_with(a, ca, ga, hl);
+        const bool done = valid && e.over();
+        if (valid && hl == 0) {
+            ((uint8_t*)out.player)[row] = (uint8_t)p;
+            ((int16_t*)out.action)[row] = (int16_t)a;
+            float r[3] = {0.f, 0.f, 0.f};
+            if (done) payoffs(e, r);
+            float* o = (float*)out.reward + row * P;
+            o[0] = r[0]; o[1] = r[1]; o[2] = r[2];
+            ((uint8_t*)out.done)[row] = (uint8_t)done;
+        }
+        const uint64_t fin = __ballot(done);
+        if (fin) {
+            if (out.final_obs) {   // Env.run's final state of every player (envs/env.py:161-164)
+                for (uint32_t q = 0; q < (uint32_t)P; q++) {
+                    wave_sync_lds();
+                    build_obs2(e, q, L, lane);
+                    wave_sync_lds();
+                    write_rows2(L, done ? (uint8_t*)out.final_obs + (row * P + q) * OBS : nullptr, nullptr, lane);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 2; j++)
+                if ((fin >> (HW * j)) & 1u) deal_half<PHX>(j, e, dlo, dhi, pm, mt, env, lane);
+        }
+    }
+    if (valid) {
+        if (hl == 0) {
+            uint4* o = (uint4*)(st + env * WORDS);
+            o[0] = make_uint4((uint32_t)e.h0, (uint32_t)(e.h0 >> 32), (uint32_t)e.h1, (uint32_t)(e.h1 >> 32));
+            o[1] = make_uint4((uint32_t)e.h2, (uint32_t)(e.h2 >> 32), (uint32_t)e.q0, (uint32_t)(e.q0 >> 32));
+            o[2] = make_uint4((uint32_t)e.q1, (uint32_t)(e.q1 >> 32), (uint32_t)e.q2, (uint32_t)(e.q2 >> 32));
+            o[3] = make_uint4(e.hw0, e.hw1, e.hw2, e.hw3);
+            o[4] = make_uint4((e.hw4 & 0xFFFFu) | (e.ggrp << 16), e.ntrace, e.greater | (e.gplay << 16),
+                              e.cur | (e.winner << 8));
+            ctl[env] = pm.pos | (pm.stale << 16) | (PHX ? CTL_PHX : 0u);
+            if constexpr (PHX) mt[env * MT_WORDS + 2] = pm.dabs;
+        }
+        uint8_t* db = (uint8_t*)(st + env * WORDS + W_DECK);
+        db[hl] = (uint8_t)dlo;
+        db[HW + hl] = (uint8_t)dhi;
+    }
+}
+
 // Test hook (cs_debug_ddz_legal): the legal set of player 0 holding `counts` -- leading when prev < 0, else following
 // another player's play `prev` -- through the same cand_of / build_legal the step and rollout kernels run (reference:
 // Judger.playable_cards_from_hand, judger.py:124-258, and get_gt_cards, utils.py:225-262, pass included)
@@ -902,6 +1389,16 @@ hipError_t launch_observe(const Buffers& b, int32_t p, const cs_step_out& o, hip
 hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
                           const cs_traj_out& o, hipStream_t s)
 {
+    if constexpr (CS_DDZ_PAIR) {
+        const dim3 g((unsigned)((b.n + 2 * PWPB - 1) / (2 * PWPB)));
+        if (b.rng_mode == CS_RNG_PHILOX)
+            hipLaunchKernelGGL(k_rollout2<true>, g, dim3(PBLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0, env_base, o,
+                               *(const Tab*)b.table);
+        else
+            hipLaunchKernelGGL(k_rollout2<false>, g, dim3(PBLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0, env_base, o,
+                               *(const Tab*)b.table);
+        return hipGetLastError();
+    }
     if (b.rng_mode == CS_RNG_PHILOX)
         hipLaunchKernelGGL(k_rollout<true>, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0, env_base, o,
                            *(const Tab*)b.table);

@@ -12,6 +12,7 @@
 #   profile:GAME[:ARGS...]    kernel trace + stats, then FETCH_SIZE and WRITE_SIZE passes over bench.py
 #   ab:GAME:N:T:F1[:F2...]    tools/ab_rollout.py kernel-flag A/B (AB_PLAYERS / AB_WARM from the env)
 #   abl:GAME:N:T:LIB1[:LIB2]  the same rollout timed with several library builds (CARDSIM_LIB), interleaved runs
+#   ceiling                   plain read / write streams and torch fill_ on this box (tools/calib.py --ceiling)
 set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -84,6 +85,9 @@ for step in "$@"; do
         done
       done
       cat "$O/abl_$g.log" ;;
+    ceiling)
+      run 300 "$O/ceiling.json" python3 tools/calib.py --ceiling
+      cat "$O/ceiling.json" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
