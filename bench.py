@@ -35,11 +35,12 @@ MT_N = 624              # words per MT19937 block
 # stream geometry (draws before the first refill, draws per refill) comes from the built library (VecEnv.rng_period:
 # the byte ring's CS_RING_SLOTS, or DouDizhu's two-block word window), see precondition_launches.
 # Fused steps per launch, measured on one box: Leduc 256 vs 128 +3 % (T >= 256), 512 vs 256 -9 %;
-# Limit / No-limit 512 vs 256 +1.5 % (round 3; 256 vs 128 +1.5 / +2 %), DouDizhu 128 vs 64 -5 % (two-env kernel).
+# Limit / No-limit 512 vs 256 +1.5 % (round 3; 256 vs 128 +1.5 / +2 %), DouDizhu 128 vs 64 -5 %, 32 vs 64 -2 % (two-env
+# kernel), Blackjack 128 vs 64 +2 %.
 GAMES = {
     'leduc-holdem': dict(envs=1 << 20, T=256, state_bytes=2 * 4 + 4, draws_per_step=2.83),
     'limit-holdem': dict(envs=262144, T=512, state_bytes=12 * 4 + 4, draws_per_step=24.5),
-    'blackjack': dict(envs=1 << 20, T=64, state_bytes=20 * 4 + 4, draws_per_step=57.0),
+    'blackjack': dict(envs=1 << 20, T=128, state_bytes=20 * 4 + 4, draws_per_step=57.0),
     'doudizhu': dict(envs=65536, T=64, state_bytes=36 * 4 + 4, draws_per_step=1.21),
     # not a BASELINE config; draws/step counted on the oracle (4096 envs x 256 random steps)
     'no-limit-holdem': dict(envs=262144, T=512, state_bytes=4 * 4 + 4, draws_per_step=26.3),
