@@ -876,19 +876,26 @@ __device__ __forceinline__ uint64_t hshfl64(uint64_t v, int lane, uint32_t k)
 // mask dword d of the shifted image (byte 16 + mis + 4 d: mis even, so 4- or 2-byte aligned)
 __device__ __forceinline__ void put_mask(PairLds& L, uint32_t d, uint32_t mis, uint32_t v)
 {
-    const uint32_t b = 16u + mis + 4u * d;
-    if ((b & 3u) == 0u) {
-        L.mask[b >> 2] = v;
-    } else {
-        uint16_t* h = (uint16_t*)L.mask + (b >> 1);
-        h[0] = (uint16_t)v;
-        h[1] = (uint16_t)(v >> 16);
-    }
+    uint16_t* h = (uint16_t*)L.mask + ((16u + mis + 4u * d) >> 1);   // two 16-bit stores: no branch on the alignment
+    h[0] = (uint16_t)v;
+    h[1] = (uint16_t)(v >> 16);
 }
 __device__ __forceinline__ uint32_t get_mask(const PairLds& L, uint32_t d, uint32_t mis)
 {
     const uint32_t b = 16u + mis + 4u * d;
     return __builtin_amdgcn_alignbyte(L.mask[(b >> 2) + 1], L.mask[b >> 2], b & 3u);
+}
+
+// inclusive prefix sum within each half-wave, with DPP (no LDS): row_shr 1, 2, 4, 8 inside the 16-lane rows, then
+// row_bcast:15 adds the last lane of rows 0 / 2 to rows 1 / 3 (row mask 0xA: rows 0 and 2 take 0)
+__device__ __forceinline__ uint32_t scan32(uint32_t x)
+{
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    return x;
 }
 
 // pass c (see build_legal) for the listed dwords [t0, lim) of each half's env, up to 4 per env
@@ -1029,12 +1036,7 @@ __device__ __forceinline__ uint32_t kth_legal2(uint32_t k, const Legal& r, PairL
         const uint32_t d = in ? L.lst[hl] : 0u;
         const uint32_t w = in ? get_mask(L, d, mis) : 0u;
         const uint32_t pc = (uint32_t)__popc(w);
-        uint32_t inc = pc;
-#pragma unroll
-        for (int o = 1; o < HW; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)inc, o, HW);
-            if (hl >= o) inc += y;
-        }
+        const uint32_t inc = scan32(pc);
         const uint32_t jm = half32(__ballot(inc > k), lane);
         const uint32_t j = jm ? (uint32_t)__builtin_ctz(jm) : 0u;
         const uint32_t incj = hshfl(inc, lane, j), pcj = hshfl(pc, lane, j), wj = hshfl(w, lane, j), dj = hshfl(d, lane, j);
