@@ -1091,16 +1091,6 @@ __device__ __forceinline__ void build_obs2(const Env& e, uint32_t self, PairLds&
     L.u.o.bv[hl] = hl == 0 ? v << 16 : v | keep32(d1 < 32u, 1u << (d1 & 31u)) | keep32(d2 < 32u, 1u << (d2 & 31u));
 }
 
-// the rows' 16-B chunks: default-policy stores (CS_DDZ_ROW_NT=1: nontemporal, as the lane-per-env games' spans)
-#ifndef CS_DDZ_ROW_NT
-#define CS_DDZ_ROW_NT 0
-#endif
-__device__ __forceinline__ void pair_store16(uint4* p, const uint4& v)
-{
-    if constexpr (CS_DDZ_ROW_NT) out_store16(p, v);
-    else *p = v;
-}
-
 // write_rows for each half's env
 __device__ __forceinline__ void write_rows2(const PairLds& L, uint8_t* orow, uint8_t* lrow, int lane)
 {
@@ -1110,7 +1100,7 @@ __device__ __forceinline__ void write_rows2(const PairLds& L, uint8_t* orow, uin
 #pragma unroll
         for (int j = 0; j < 2; j++) {
             const int q = j * HW + hl;
-            if (q >= 1 && q < nchunks - 1) pair_store16((uint4*)(orow - mis + 16 * q), obs_chunk(L.u.o.bv, q, mis));
+            if (q >= 1 && q < nchunks - 1) *(uint4*)(orow - mis + 16 * q) = obs_chunk(L.u.o.bv, q, mis);
         }
     }
     if (lrow) {   // chunk q = image block q + 1 (the image is shifted by the row's misalignment)
@@ -1118,7 +1108,7 @@ __device__ __forceinline__ void write_rows2(const PairLds& L, uint8_t* orow, uin
 #pragma unroll CS_DDZ_LROW_UNROLL
         for (int j = 0; j < (216 + HW - 1) / HW; j++) {
             const int q = j * HW + hl;
-            if (q >= 1 && q < nchunks - 1) pair_store16((uint4*)(lrow - mis + 16 * q), ((const uint4*)L.mask)[q + 1]);
+            if (q >= 1 && q < nchunks - 1) *(uint4*)(lrow - mis + 16 * q) = ((const uint4*)L.mask)[q + 1];
         }
     }
     // the rows' end chunks, a byte per lane: lanes 0..15 / 16..31 of a half the first / last chunk
