@@ -1,4 +1,8 @@
-"""Blackjack env (rlcard/envs/blackjack.py:38-103) over the HIP engine (rlcard_amd/csrc/cs_blackjack.h)."""
+"""Blackjack env (rlcard/envs/blackjack.py:38-103) over the HIP engine (rlcard_amd/csrc/cs_blackjack.h).
+
+step_back restores the whole game and continues the env's stream; the reference's Game.step_back (game.py:65-70,
+125-135) restores a deep copy of the dealer with its RandomState, so its next hits redraw the undone cards, and puts
+the acting player's snapshot into the current pointer's seat."""
 import numpy as np
 
 from .env import Env
