@@ -93,6 +93,15 @@ std::string table_build_host(std::vector<uint8_t>& host, size_t off[4], Tab* tab
     }
     if (type_lo[TYPE_BOMB] < 0 || type_lo[TYPE_ROCKET] < 0 || type_hi[TYPE_ROCKET] != type_lo[TYPE_ROCKET] + 1)
         return "doudizhu table: bomb / rocket ranges not found";
+    // the kernels compute the packed counts and groups of the simple ids (cs_doudizhu.h simple_cnt / simple_gid)
+    const uint32_t blo = (uint32_t)type_lo[TYPE_BOMB], bg = gid[blo];
+    if (type_hi[TYPE_BOMB] != (int)blo + 13 || type_lo[TYPE_ROCKET] != (int)blo + 13)
+        return "doudizhu table: bombs and rocket are not 14 consecutive ids";
+    for (uint32_t id = 0; id < (uint32_t)PASS; id++) {
+        if (!simple_id(id, blo)) continue;
+        if (cnt[id] != simple_cnt(id, blo) || gid[id] != simple_gid(id, blo, bg))
+            return "doudizhu table: solo / pair / trio / bomb / rocket ids out of the kernels' layout";
+    }
 
     // one device allocation: cnt | gid | grp | drange
     const size_t o_cnt = 0, o_gid = o_cnt + (size_t)NA * 8, o_grp = (o_gid + (size_t)NA * 2 + 255) & ~(size_t)255,
@@ -107,6 +116,7 @@ std::string table_build_host(std::vector<uint8_t>& host, size_t off[4], Tab* tab
     tab->bomb_lo = type_lo[TYPE_BOMB];
     tab->bomb_hi = type_hi[TYPE_BOMB];
     tab->rocket = type_lo[TYPE_ROCKET];
+    tab->bomb_g = (int32_t)bg;
     for (int k = 0; k <= MAX_GROUPS / 32; k++) tab->kfirst[k] = 32 * k < ng ? gstart[32 * k] : PASS;
     return "";
 }

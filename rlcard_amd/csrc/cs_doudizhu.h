@@ -46,10 +46,35 @@ struct Tab {
     const uint32_t* drange;  // [ND]
     int32_t ng;
     int32_t bomb_lo, bomb_hi, rocket;
+    int32_t bomb_g;          // group of the first bomb (bombs and the rocket: groups bomb_g .. bomb_g + 13)
     // kfirst[k]: the first id of group 32 k (PASS past the last group): the ids of groups 32 k .. 32 k + 31 lie in
     // [kfirst[k], kfirst[k + 1]), so a 32-group pass of the legal scan that no candidate range meets is skipped
     int32_t kfirst[MAX_GROUPS / 32 + 1];
 };
+
+// "Simple" ids, whose packed counts and group the kernels compute instead of loading them from the table (checked by
+// the table builder): solo / pair / trio of rank r = ids r / 15 + r / 28 + r (groups = ids), bomb of rank r = bomb_lo
+// + r, the rocket (groups bomb_g + r, bomb_g + 13).
+constexpr uint32_t SIMPLE_HI = 41;
+#ifdef __HIPCC__
+#define CS_DDZ_HD __host__ __device__ __forceinline__
+#else
+#define CS_DDZ_HD inline
+#endif
+CS_DDZ_HD bool simple_id(uint32_t id, uint32_t bomb_lo)
+{
+    return id < SIMPLE_HI || id - bomb_lo <= 13u;
+}
+CS_DDZ_HD uint64_t simple_cnt(uint32_t id, uint32_t bomb_lo)
+{
+    const uint32_t k = id < 15u ? 1u : (id < 28u ? 2u : (id < SIMPLE_HI ? 3u : 4u));
+    const uint32_t r = id < 15u ? id : (id < 28u ? id - 15u : (id < SIMPLE_HI ? id - 28u : id - bomb_lo));
+    return r == 13u && id >= SIMPLE_HI ? (1ull << 52 | 1ull << 56) : (uint64_t)k << (4u * r);
+}
+CS_DDZ_HD uint32_t simple_gid(uint32_t id, uint32_t bomb_lo, uint32_t bomb_g)
+{
+    return id < SIMPLE_HI ? id : bomb_g + (id - bomb_lo);
+}
 
 // Packed env state (u32 words, env-major: st[env * WORDS + w]):
 //   0..5   hand[p]   packed counts, p = 0 (landlord), 1, 2     (lo, hi)

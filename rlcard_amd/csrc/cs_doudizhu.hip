@@ -848,8 +848,18 @@ constexpr int NCH = (ND + HW - 1) / HW;              // 27 chunks of 32 mask dwo
 // The pair kernel keeps the legal mask image SHIFTED by the legal row's misalignment mis (row byte o at image byte
 // 16 + mis + o), so the row's 16-B chunks are aligned 16-B blocks of the image (ds_read_b128, no bank conflicts, no
 // byte alignment); a mask dword is written / read at byte 16 + mis + 4 d (2-byte aligned: mis is even).
+// the image padded to whole 16-B stores of 32 lanes: the per-step zeroing runs unpredicated, so every store takes the
+// same zero register (predicated, the compiler kept a second zero in a scratch spill whose reload waited on vmcnt(0)
+// -- every row store of the previous step -- at the top of each step)
+#ifndef CS_DDZ_PAD
+#define CS_DDZ_PAD 1
+#endif
+#ifndef CS_DDZ_SIMPLE
+#define CS_DDZ_SIMPLE 1   // bit 0: the fast path's candidates, bit 1: the chosen action's entries from simple_cnt / _gid (bit 1 measured 11 % slower: the select puts the table load's wait before the row stores)
+#endif
+constexpr int PMASK_WORDS = CS_DDZ_PAD ? (MASK_WORDS / 4 + HW - 1) / HW * HW * 4 : MASK_WORDS;
 struct alignas(16) PairLds {
-    uint32_t mask[MASK_WORDS];                       // the shifted image (see above)
+    uint32_t mask[PMASK_WORDS];                      // the shifted image (see above)
     union {
         uint16_t pre[MAX_GROUPS + 8];                // the legal scan's group prefix counts, dead once it is done:
         struct {                                     // the obs image reuses the space
@@ -923,7 +933,71 @@ __device__ __forceinline__ void test_listed2(uint32_t t0, uint32_t lim, uint64_t
     }
 }
 
-// build_legal for each half's env (act: the half holds a live env); the mask image must be zero on entry
+// Following a play the candidates are at most three id ranges (cand_of: the same type's greater weights, the bombs, the
+// rocket). In random play they number <= 32 in ~93 % of the following steps (~70 % of all steps; the same-type range
+// has median 5 ids, p90 14), and then the half's 32 lanes test one candidate each -- no group pass, no chunk pass, no
+// listed-dword batches. Lane k takes the k-th candidate in id order (the table's bomb and rocket types are its last
+// ids, so the ranges come in the order same type < bombs < rocket); the dwords holding a legal id are listed in order
+// (the group path lists every dword it tests; kth_legal2 only sums their popcounts) and the legal bits OR-ed into the
+// shifted image through 32 scratch dwords (the upper half of the list: this path lists at most 32 dwords). Same image,
+// same legal count. Two parts: fast_issue loads the candidates' packed counts from the table in HBM / L2 at the start
+// of the step, fast_finish tests them after the group pass (other half) and build_obs2, which hide the load latency
+// (issued and tested back to back the path measured slower than the group pass it replaces). The solo / pair / trio /
+// bomb / rocket candidates (~95 % of these steps have no other) take their counts from simple_cnt: no load.
+#ifndef CS_DDZ_FAST_FOLLOW
+#define CS_DDZ_FAST_FOLLOW 1
+#endif
+struct Fast {
+    bool fast, cand, load;   // load: a candidate that is not a simple id (its counts come from the table)
+    uint32_t id;
+    uint64_t cnt;
+};
+__device__ __forceinline__ Fast fast_issue(const Env& e, const Cand& c, const Tab& tb, PairLds& L, int lane, bool act)
+{
+    const uint32_t hl = (uint32_t)(lane & (HW - 1));
+    Fast f;
+    f.fast = CS_DDZ_FAST_FOLLOW != 0 && act && !e.over() && !c.leading && c.c_len + c.b_len + c.r_len <= (uint32_t)HW;
+    const uint32_t n0 = c.c_len, n1 = n0 + c.b_len, n2 = n1 + c.r_len;
+    f.cand = f.fast && hl < n2;
+    f.id = hl < n0 ? c.c_lo + hl : (hl < n1 ? c.b_lo + (hl - n0) : c.r_lo + (hl - n1));
+    const bool simple = (CS_DDZ_SIMPLE & 1) && simple_id(f.id, (uint32_t)tb.bomb_lo);
+    f.load = f.cand && !simple;
+    f.cnt = f.cand && simple ? simple_cnt(f.id, (uint32_t)tb.bomb_lo) : ~0ull;
+    if (f.fast) ((uint32_t*)L.lst)[HW + hl] = 0u;   // the OR scratch: list entries 64..127
+    return f;
+}
+__device__ __forceinline__ void fast_finish(const Fast& f, uint64_t h, const Tab& tb, PairLds& L, uint32_t mis, int lane,
+                                            Legal& r)
+{
+    const uint32_t hl = (uint32_t)(lane & (HW - 1));
+    uint32_t* scr = (uint32_t*)L.lst + HW;
+    uint64_t cnt = f.cnt;
+    // table loads only where a candidate is not simple (~5 % of these steps), waited for inside this branch: on gfx950
+    // a load's wait also waits for every earlier store (vmcnt counts both), here the previous step's row stores
+    if (__ballot(f.load)) cnt = f.load ? tb.cnt[f.id] : cnt;
+    const bool pass = f.cand && contains(h, cnt);
+    const uint32_t m = half32(__ballot(pass), lane);
+    const uint32_t dw = f.id >> 5;
+    const uint32_t below = m & ((1u << hl) - 1u);                   // legal candidates before this lane's
+    const uint32_t pdw = hshfl(dw, lane, below ? 31u - (uint32_t)__builtin_clz(below) : hl);
+    const bool first = pass && (below == 0u || pdw != dw);           // the first legal id of its dword
+    const uint32_t fm = half32(__ballot(first), lane);
+    const uint32_t k = (uint32_t)__popc(fm & ((2u << hl) - 1u)) - 1u;   // its dword's rank in the list
+    wave_sync_lds();
+    if (pass) atomicOr(scr + k, 1u << (f.id & 31u));
+    wave_sync_lds();
+    if (first) {
+        put_mask(L, dw, mis, scr[k]);
+        L.lst[k] = (uint16_t)dw;
+    }
+    if (f.fast) {
+        r.total = (uint32_t)__popc(m);
+        r.nl = (uint32_t)__popc(fm);
+    }
+}
+
+// build_legal for each half's env (act: the half holds a live env that does not take the fast path); the mask image
+// must be zero on entry
 __device__ __forceinline__ Legal build_legal2(const Env& e, const Cand& c, const Tab& tb, const TabLds& T, PairLds& L,
                                               uint32_t mis, int lane, bool act)
 {
@@ -1162,7 +1236,7 @@ __device__ __forceinline__ void deal_half(int j, Env& e, uint32_t& dlo, uint32_t
 template <bool PHX>
 __global__ __launch_bounds__(PBLOCK, CS_DDZ_PAIR_MINW) void k_rollout2(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n, int T,
                                                      uint64_t seed, uint64_t t0, uint64_t env_base, cs_traj_out out,
-                                                     Tab tb)
+                                                     Tab tb, int kfl)
 {
     __shared__ PairLds lds[PWPB][2];
     __shared__ TabLds tl;
@@ -1231,19 +1305,21 @@ __global__ __launch_bounds__(PBLOCK, CS_DDZ_PAIR_MINW) void k_rollout2(uint32_t*
     uint32_t rr_lane = 0;
     for (int t = 0; t < T; t++) {
         const int64_t row = (int64_t)t * n + env;
-        {   // zero the mask image of both envs: 218 uint4 each, 32 lanes per env
+        {   // zero the mask image of both envs: 224 uint4 each, 32 lanes per env
             uint4* z = (uint4*)L.mask;
 #pragma unroll
-            for (int j = 0; j < (MASK_WORDS / 4 + HW - 1) / HW; j++) {
+            for (int j = 0; j < (PMASK_WORDS / 4 + HW - 1) / HW; j++) {
                 const int q = j * HW + hl;
-                if (q < MASK_WORDS / 4) z[q] = make_uint4(0, 0, 0, 0);
+                if (CS_DDZ_PAD || q < PMASK_WORDS / 4) z[q] = make_uint4(0, 0, 0, 0);
             }
         }
         wave_sync_lds();
         const uint32_t lmis = (uint32_t)(((uintptr_t)out.legal + (uint64_t)row * LB) & 15u);   // the image's shift
         const Cand cd = cand_of(e, tb, tl);
-        const Legal lg = build_legal2(e, cd, tb, tl, L, lmis, lane, valid);
+        const Fast fst = fast_issue(e, cd, tb, L, lane, valid && (kfl & 1) == 0);   // kernel flag bit 0: A/B only
+        Legal lg = build_legal2(e, cd, tb, tl, L, lmis, lane, valid && !fst.fast);
         build_obs2(e, e.cur, L, lane);
+        if (__ballot(fst.fast)) fast_finish(fst, e.hand(e.cur), tb, L, lmis, lane, lg);
         wave_sync_lds();
         const uint32_t count = lg.total + (cd.leading ? 0u : 1u);
         if ((t & (HW - 1)) == 0) rr_lane = philox_u32(seed, genv, t0 + (uint64_t)(t + hl));
@@ -1251,8 +1327,9 @@ __global__ __launch_bounds__(PBLOCK, CS_DDZ_PAIR_MINW) void k_rollout2(uint32_t*
         const uint32_t a = kth_legal2((uint32_t)(((uint64_t)rr * count) >> 32), lg, PL, lmis, lane);
         // the action's table entries, loaded now so that their latency hides behind the row writes
         const bool play = valid && a != (uint32_t)PASS;
-        const uint64_t ca = play ? tb.cnt[a] : 0ull;
-        const uint32_t ga = play ? (uint32_t)tb.gid[a] : 0u;
+        const bool sa = (CS_DDZ_SIMPLE & 2) && simple_id(a, (uint32_t)tb.bomb_lo);
+        const uint64_t ca = play ? (sa ? simple_cnt(a, (uint32_t)tb.bomb_lo) : tb.cnt[a]) : 0ull;
+        const uint32_t ga = play ? (sa ? simple_gid(a, (uint32_t)tb.bomb_lo, (uint32_t)tb.bomb_g) : (uint32_t)tb.gid[a]) : 0u;
         if (valid && !cd.leading && hl == 0) ((uint8_t*)L.mask)[16u + lmis + PASS / 8] |= (uint8_t)(1u << (PASS & 7));
         wave_sync_lds();
         write_rows2(L, valid && !(CS_PROF_DDZ & 2) ? (uint8_t*)out.obs + row * OBS : nullptr,
@@ -1395,10 +1472,10 @@ hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t
         const dim3 g((unsigned)((b.n + 2 * PWPB - 1) / (2 * PWPB)));
         if (b.rng_mode == CS_RNG_PHILOX)
             hipLaunchKernelGGL(k_rollout2<true>, g, dim3(PBLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0, env_base, o,
-                               *(const Tab*)b.table);
+                               *(const Tab*)b.table, b.serial_refill);
         else
             hipLaunchKernelGGL(k_rollout2<false>, g, dim3(PBLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0, env_base, o,
-                               *(const Tab*)b.table);
+                               *(const Tab*)b.table, b.serial_refill);
         return hipGetLastError();
     }
     if (b.rng_mode == CS_RNG_PHILOX)
