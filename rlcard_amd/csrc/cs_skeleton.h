@@ -160,6 +160,20 @@ template <class G>
 struct RewardPairs {
     static constexpr bool value = CS_REWARD_PAIRS && G::P == 2;
 };
+// CS_REWARD_PAIRS=2: the wave's 2 x EPW reward dwords transposed so that lane l stores dword l (and 64 + l): fully
+// coalesced 4-B stores (4 ds_bpermute per step)
+template <int EPW>
+__device__ __forceinline__ void emit_reward_t(float* reward, int64_t rowbase, const float (&r)[2], const LaneCtx& c)
+{
+    const uint32_t a0 = __float_as_uint(r[0]), a1 = __float_as_uint(r[1]);
+    uint32_t* dst = (uint32_t*)(reward + (rowbase + c.wave_first) * 2);
+#pragma unroll
+    for (int h = 0; h < (2 * EPW + WAVE - 1) / WAVE; h++) {
+        const int d = h * WAVE + c.lane, src = d >> 1;
+        const uint32_t x = __builtin_amdgcn_ds_bpermute(src << 2, (int)a0), y = __builtin_amdgcn_ds_bpermute(src << 2, (int)a1);
+        if (d < 2 * EPW && src < c.nvalid) out_store(dst + d, (d & 1) ? y : x);
+    }
+}
 template <int P>
 __device__ __forceinline__ void emit_reward_pairs(float* reward, int64_t rowbase, const float (&r)[P],
                                                   const LaneCtx& c)
@@ -583,9 +597,17 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
 #ifndef CS_PROF_NO_OBS   // profiling builds only (tools: make variant DEFS=-DCS_PROF_NO_OBS): outputs incomplete
         emit_obs<G, G::EPW>(lds[c.wid], bits, obs, rowbase + c.wave_first, flags, c);
 #endif
+        // the reward row starts from a zero the compiler cannot hoist out of the loop: a loop-invariant zero pair was
+        // kept in a scratch spill whose reload, before each step's reward store, waited on vmcnt(0) -- on gfx950 every
+        // store the wave had issued (the obs rows): a drain per step
+        uint32_t zr = 0;
+#ifndef CS_ZERO_OPAQUE
+#define CS_ZERO_OPAQUE 1
+#endif
+        if constexpr (CS_ZERO_OPAQUE != 0) asm volatile("" : "+v"(zr));
         float r[G::P];
 #pragma unroll
-        for (int k = 0; k < G::P; k++) r[k] = 0.f;
+        for (int k = 0; k < G::P; k++) r[k] = __uint_as_float(zr);
         bool done = false;
         if (c.valid) {
             const int64_t row = rowbase + c.env;
@@ -617,7 +639,10 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
             }
         }
 #ifndef CS_PROF_NO_SMALL
-        if constexpr (RewardPairs<G>::value) emit_reward_pairs(reward, rowbase, r, c);
+        if constexpr (RewardPairs<G>::value) {
+            if constexpr (CS_REWARD_PAIRS == 2) emit_reward_t<G::EPW>(reward, rowbase, r, c);
+            else emit_reward_pairs(reward, rowbase, r, c);
+        }
 #endif
         if constexpr (DQ > 0) {
             // a lane ending its game with an empty queue makes every lane with room draw one deal ahead, in lockstep
