@@ -548,6 +548,12 @@ struct RowWriter {
 #pragma unroll
             for (int j = 0; j < DW; j++) lds[lane * DW + j] = expand4(bits[j / 8] >> (4 * (j % 8)));
         }
+        write_out(lds, bits, out_span, lane, nvalid, wide);
+    }
+    // the span image in LDS (written by this wave) to the output span
+    __device__ static __forceinline__ void write_out(uint32_t* lds, const uint32_t (&)[NB], uint8_t* out_span,
+                                                     int lane, int nvalid, bool wide)
+    {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -597,6 +603,10 @@ struct RowWriterRaw {
                 for (int j = 0; j < ROW / 2; j++) l16[j] = (uint16_t)(words[j / 2] >> (16 * (j & 1)));
             }
         }
+        write_out(lds, out_span, lane, nvalid, wide);
+    }
+    __device__ static __forceinline__ void write_out(uint32_t* lds, uint8_t* out_span, int lane, int nvalid, bool wide)
+    {
         wave_sync_lds();
         const int bytes = nvalid * ROW;
         if (SPAN % 16 == 0 && wide && nvalid == ROWS && (((uintptr_t)out_span) & 15u) == 0) {
@@ -618,6 +628,40 @@ struct RowWriterRaw {
         wave_sync_lds();
     }
 };
+
+// The span writer for one-hot rows with few ones at known positions (Leduc: K = 4 byte positions per row, a repeated
+// position for an absent one): the lanes zero the span image with 16-B LDS stores, then write their K ones as byte
+// stores (a wave's LDS operations complete in order), instead of expanding every dword of the row (4 VALU + one LDS
+// store per dword). The span leaves LDS exactly as write() sends it.
+// RAW: the row is raw bytes (RowWriterRaw) whose last two bytes are the 16-bit value `tail` (No-limit's chips); the
+// ones sit among the bytes before them.
+template <int ROW, int ROWS, int K, bool RAW = false>
+__device__ __forceinline__ void row_write_sparse(uint32_t* lds, const uint32_t (&pos)[K], uint8_t* out_span, int lane,
+                                                 int nvalid, bool wide, uint32_t tail = 0)
+{
+    constexpr int SPAN16 = (ROWS * ROW + 15) / 16;
+    uint4* z = (uint4*)lds;
+    uint32_t zero = 0;
+    asm volatile("" : "+v"(zero));   // made here: a hoisted zero register ends up in a scratch spill (vmcnt(0) reload)
+#pragma unroll
+    for (int j = 0; j < (SPAN16 + WAVE - 1) / WAVE; j++) {
+        const int q = j * WAVE + lane;
+        if (q < SPAN16) z[q] = make_uint4(zero, zero, zero, zero);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane < ROWS) {
+        uint8_t* row = (uint8_t*)lds + lane * ROW;
+#pragma unroll
+        for (int k = 0; k < K; k++) row[pos[k]] = 1;
+        if constexpr (RAW) *(uint16_t*)(row + ROW - 2) = (uint16_t)tail;   // ROW even: 2-B aligned
+    }
+    if constexpr (RAW) {
+        RowWriterRaw<ROW, ROWS>::write_out(lds, out_span, lane, nvalid, wide);
+    } else {
+        uint32_t none[RowWriter<ROW, ROWS>::NB];
+        RowWriter<ROW, ROWS>::write_out(lds, none, out_span, lane, nvalid, wide);
+    }
+}
 
 // set bit p of a multi-word bitmap without dynamic register indexing
 template <int NB>

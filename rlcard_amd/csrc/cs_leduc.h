@@ -33,6 +33,9 @@
 #ifndef CS_LEDUC_MIN_WAVES
 #define CS_LEDUC_MIN_WAVES 6
 #endif
+#ifndef CS_LEDUC_SPARSE_OBS
+#define CS_LEDUC_SPARSE_OBS 1   // rollout obs rows through row_write_sparse (0: the expanded bitmap, RowWriter)
+#endif
 #ifndef CS_LEDUC_STAGE_W
 #define CS_LEDUC_STAGE_W 64
 #endif
@@ -97,6 +100,19 @@ struct Leduc {
         if (rc >= 1) b |= 1ull << ((pub >> 1) + 3);
         bits[0] = (uint32_t)b;
         bits[1] = (uint32_t)(b >> 32);
+    }
+
+    // the same row as the byte positions of its ones (row_write_sparse): hand rank, public rank + 3 (absent: the hand
+    // position again), my chips + 6, the others' chips + 21
+    static constexpr int SPARSE_K = CS_LEDUC_SPARSE_OBS ? 4 : 0;
+    __device__ __forceinline__ uint32_t observe_pos(int player, uint32_t (&pos)[4]) const
+    {
+        const int my = player ? in1 : in0, hand = (player ? h1 : h0) >> 1;
+        pos[0] = (uint32_t)hand;
+        pos[1] = (uint32_t)(rc >= 1 ? (pub >> 1) + 3 : hand);
+        pos[2] = (uint32_t)(my + 6);
+        pos[3] = (uint32_t)(in0 + in1 - my + 21);
+        return 0;
     }
 
     // dealer.py shuffle (intervals 5..1, swap) then randint(0, 2) for the small blind: six random_interval draws as

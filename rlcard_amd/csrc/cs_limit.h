@@ -43,6 +43,9 @@
 #ifndef CS_LIMIT_DQ_REGS
 #define CS_LIMIT_DQ_REGS 0
 #endif
+#ifndef CS_LIMIT_SPARSE_OBS
+#define CS_LIMIT_SPARSE_OBS 1   // rollout obs rows through row_write_sparse (0: the expanded bitmap, RowWriter)
+#endif
 #ifndef CS_LIMIT_EPW
 #define CS_LIMIT_EPW 32
 #endif
@@ -473,6 +476,23 @@ struct Limit {
         bits[0] = (uint32_t)cm;
         bits[1] = (uint32_t)(cm >> 32) | R << 20;
         bits[2] = R >> 12;
+    }
+
+    // the same row as the byte positions of its 11 ones (row_write_sparse): the two holes, the five board cards (not
+    // yet public: the first hole again), obs byte 52 + 5 i + raise count of round i (i = 0..3)
+    static constexpr int SPARSE_K = CS_LIMIT_SPARSE_OBS ? 11 : 0;
+    __device__ __forceinline__ uint32_t observe_pos(int player, uint32_t (&pos)[11]) const
+    {
+        const int r = rc(), npub = r == 0 ? 0 : (r == 1 ? 3 : (r == 2 ? 4 : 5));
+        const uint32_t c0 = (uint32_t)hole(player, 0);
+        pos[0] = c0;
+        pos[1] = (uint32_t)hole(player, 1);
+#pragma unroll
+        for (int k = 0; k < 5; k++) pos[2 + k] = k < npub ? (uint32_t)board(k) : c0;
+        const uint32_t rn = use_prev() ? (w3 >> 12) : w3;
+#pragma unroll
+        for (int i = 0; i < 4; i++) pos[7 + i] = 52u + 5u * (uint32_t)i + ((rn >> (3 * i)) & 7u);
+        return 0;
     }
 
     // the deal of init_game (game.py:46-95): shuffle + holes + board, then the small blind seat randint(0, 2)

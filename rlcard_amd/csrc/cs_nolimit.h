@@ -40,6 +40,9 @@
 #ifndef CS_NOLIMIT_DQ_REGS
 #define CS_NOLIMIT_DQ_REGS 0
 #endif
+#ifndef CS_NOLIMIT_SPARSE_OBS
+#define CS_NOLIMIT_SPARSE_OBS 1   // rollout obs rows through row_write_sparse (0: RowWriterRaw of the expanded row)
+#endif
 #ifndef CS_NOLIMIT_EPW
 #define CS_NOLIMIT_EPW 32
 #endif
@@ -131,6 +134,21 @@ struct Nolimit {
         for (int j = 0; j < 13; j++) raw[j] = RowWriter<4>::expand4((uint32_t)(cards >> (4 * j)) & 15u);
         const int a = in(0), b = in(1);
         raw[13] = (uint32_t)(player ? b : a) | (uint32_t)(a > b ? a : b) << 8;
+    }
+
+    // the same row as the byte positions of its 7 card ones (row_write_sparse: the two holes, the public board cards,
+    // the first hole again for the others) and its last two bytes (my chips | the max chips << 8), returned
+    static constexpr int SPARSE_K = CS_NOLIMIT_SPARSE_OBS ? 7 : 0;
+    __device__ __forceinline__ uint32_t observe_pos(int player, uint32_t (&pos)[7]) const
+    {
+        const int r = rc(), npub = r == 0 ? 0 : (r + 2 < 5 ? r + 2 : 5);
+        const uint32_t c0 = (uint32_t)hole(player, 0);
+        pos[0] = c0;
+        pos[1] = (uint32_t)hole(player, 1);
+#pragma unroll
+        for (int k = 0; k < 5; k++) pos[2 + k] = k < npub ? (uint32_t)board(k) : c0;
+        const int a = in(0), b = in(1);
+        return (uint32_t)(player ? b : a) | (uint32_t)(a > b ? a : b) << 8;
     }
 
     // the dealer seat randint(0, 2) before the first game's shuffle (game.py:62-63; kept by later games of the env,

@@ -125,6 +125,12 @@ __device__ __forceinline__ void write_obs_direct(uint8_t* o, const uint32_t (&bi
     }
 }
 
+// games whose obs rows are one-hot with SPARSE_K known positions (observe_pos) write them with row_write_sparse
+template <class G, class = void>
+struct SparseObs : std::false_type {};
+template <class G>
+struct SparseObs<G, std::void_t<decltype(G::SPARSE_K)>> : std::bool_constant<(G::SPARSE_K > 0)> {};
+
 template <class G>
 __device__ __forceinline__ void emit_legal(uint8_t* legal, int64_t row, uint64_t lg)
 {
@@ -595,7 +601,15 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
         if constexpr (G::A <= 8) a = pick_legal_small<G::A>((uint32_t)lg, pr);
         else a = G::A <= 32 ? pick_legal32((uint32_t)lg, pr) : pick_legal(lg, pr);
 #ifndef CS_PROF_NO_OBS   // profiling builds only (tools: make variant DEFS=-DCS_PROF_NO_OBS): outputs incomplete
-        emit_obs<G, G::EPW>(lds[c.wid], bits, obs, rowbase + c.wave_first, flags, c);
+        if constexpr (SparseObs<G>::value) {   // one-hot rows with a few known positions (row_write_sparse)
+            uint32_t pos[G::SPARSE_K];
+            const uint32_t tail = g.observe_pos(p, pos);
+            row_write_sparse<G::OBS, G::EPW, G::SPARSE_K, G::RAW_OBS>(lds[c.wid], pos,
+                                                                      obs + (rowbase + c.wave_first) * G::OBS, c.lane,
+                                                                      c.nvalid, !(flags & 4), tail);
+        } else {
+            emit_obs<G, G::EPW>(lds[c.wid], bits, obs, rowbase + c.wave_first, flags, c);
+        }
 #endif
         // the reward row starts from a zero the compiler cannot hoist out of the loop: a loop-invariant zero pair was
         // kept in a scratch spill whose reload, before each step's reward store, waited on vmcnt(0) -- on gfx950 every
