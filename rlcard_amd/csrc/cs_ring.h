@@ -112,12 +112,22 @@ __device__ __attribute__((noinline)) void ring_gen_serial(uint32_t* wbuf, uint32
 // Block words in registers, word k = 64c + lane in o[c] (c = 9 holds words 576..623 in lanes 0..47). One twist:
 //   new[k] = mix(old[k], old[k+1] | new[0] (k = 623), old[k+397] (k < 227) | new[k-227])
 // with the cross-lane operands fetched by ds_bpermute; n[c] only depends on n[c-4], n[c-3] and n[0] (computed first).
+// CS_TWIST_DPP: the k+1 operand (the next lane) through a DPP wavefront shift (wave_shl:1, a VALU modifier) instead of
+// a ds_bpermute round trip through the LDS crossbar
+#ifndef CS_TWIST_DPP
+#define CS_TWIST_DPP 1
+#endif
 __device__ __forceinline__ void twist_regs(const uint32_t (&o)[10], uint32_t (&n)[10], int lane)
 {
     const int l1 = (lane + 1) & 63, l13 = (lane + 13) & 63, l29 = (lane + 29) & 63;
+    (void)l1;
 #pragma unroll
     for (int c = 0; c < 10; c++) {
-        uint32_t nxt = shfl(o[c], l1);
+        uint32_t nxt;
+        if constexpr (CS_TWIST_DPP != 0)
+            nxt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)o[c], 0x130, 0xF, 0xF, false);   // wave_shl:1
+        else
+            nxt = shfl(o[c], l1);
         if (c < 9) {
             const uint32_t wrap = __builtin_amdgcn_readlane(o[c + 1], 0);
             nxt = lane == 63 ? wrap : nxt;
