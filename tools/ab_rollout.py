@@ -13,36 +13,44 @@ from rlcard_amd import VecEnv  # noqa: E402
 
 game, n, T = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 variants = [int(x) for x in sys.argv[4:]] or [0, 2, 4, 6]
+# AB_TS=T1,T2,..: the variants are fused-step counts (kernel flags 0) instead of kernel flags; T is ignored
+Ts = [int(x) for x in os.environ.get('AB_TS', '').split(',') if x]
+if Ts:
+    variants = Ts
 np_ = int(os.environ.get('AB_PLAYERS', '0'))   # game_num_players (0: the game's default)
 inst = int(os.environ.get('AB_INST', '1'))       # fresh VecEnv allocations, variants interleaved in each (box / run
 allt = {f: [] for f in variants}                 # variance follows the allocation: compare within one)
 for i in range(inst):
     v = VecEnv(game, n, seed=42 + i, device=0, config={'game_num_players': np_} if np_ else None)
     v.reset()
-    tr = v.new_traj_out(T)
-    t = 0
+    Tv = {f: (f if Ts else T) for f in variants}
+    trs = {f: v.new_traj_out(Tv[f]) for f in variants} if Ts else None
+    tr = v.new_traj_out(T) if not Ts else trs[variants[0]]
+    t = 0   # absolute step of the policy stream
     for _ in range(int(os.environ.get('AB_WARM', '40'))):
-        v.rollout(T, 5, t * T, out=tr); t += 1
+        v.rollout(Tv[variants[0]], 5, t, out=tr); t += Tv[variants[0]]
     for f in variants:            # warm-up each variant
-        v.set_kernel_flags(f)
-        v.rollout(T, 5, t * T, out=tr); t += 1
+        if not Ts:
+            v.set_kernel_flags(f)
+        v.rollout(Tv[f], 5, t, out=trs[f] if Ts else tr); t += Tv[f]
     torch.cuda.synchronize()
     times = {f: [] for f in variants}
     for rnd in range(6):
         for f in variants:
-            v.set_kernel_flags(f)
+            if not Ts:
+                v.set_kernel_flags(f)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for k in range(5):
-                v.rollout(T, 5, t * T, out=tr); t += 1
+                v.rollout(Tv[f], 5, t, out=trs[f] if Ts else tr); t += Tv[f]
             e1.record()
             torch.cuda.synchronize()
-            times[f].append(e0.elapsed_time(e1) / 5)
+            times[f].append(e0.elapsed_time(e1) / 5 / (Tv[f] / T))   # per T steps
     for f in variants:
         allt[f] += times[f]
         if inst > 1:
             print('  instance %d flags=%d: median %.3f ms/launch' % (i, f, statistics.median(times[f])), flush=True)
-    del v, tr
+    del v, tr, trs
     torch.cuda.empty_cache()
 for f in variants:
     med = statistics.median(allt[f])
