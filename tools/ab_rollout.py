@@ -24,7 +24,9 @@ for i in range(inst):
     v = VecEnv(game, n, seed=42 + i, device=0, config={'game_num_players': np_} if np_ else None)
     v.reset()
     Tv = {f: (f if Ts else T) for f in variants}
-    trs = {f: v.new_traj_out(Tv[f]) for f in variants} if Ts else None
+    # one allocation of the largest T; smaller T launches write its leading steps (same buffers, no allocation effect)
+    big = v.new_traj_out(max(Tv.values())) if Ts else None
+    trs = {f: {k: x[:Tv[f]] for k, x in big.items()} for f in variants} if Ts else None
     tr = v.new_traj_out(T) if not Ts else trs[variants[0]]
     t = 0   # absolute step of the policy stream
     for _ in range(int(os.environ.get('AB_WARM', '40'))):
@@ -50,7 +52,7 @@ for i in range(inst):
         allt[f] += times[f]
         if inst > 1:
             print('  instance %d flags=%d: median %.3f ms/launch' % (i, f, statistics.median(times[f])), flush=True)
-    del v, tr, trs
+    del v, tr, trs, big
     torch.cuda.empty_cache()
 for f in variants:
     med = statistics.median(allt[f])
