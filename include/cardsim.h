@@ -267,8 +267,8 @@ int cs_debug_ddz_legal(cs_handle* h, const uint8_t* counts, const int32_t* prev,
 int cs_debug_set_serial_refill(cs_handle* h, int32_t enable);
 
 /* Tuning hook: kernel variant bits (bit 0 = serial MT refill; DouDizhu rollouts: every legal set through the group
- * pass, no following fast path; bit 1 = reserved, bit 2 = dword instead of 16-B obs stores). Results are identical
- * for every value. */
+ * pass, no following fast path; bit 1 = DouDizhu rollouts: the whole legal image zeroed at every step; bit 2 = dword
+ * instead of 16-B obs stores). Results are identical for every value. */
 int cs_debug_set_kernel_flags(cs_handle* h, int32_t flags);
 
 const char* cs_last_error(void);

@@ -857,6 +857,9 @@ constexpr int NCH = (ND + HW - 1) / HW;              // 27 chunks of 32 mask dwo
 #ifndef CS_DDZ_SIMPLE
 #define CS_DDZ_SIMPLE 1   // bit 0: the fast path's candidates, bit 1: the chosen action's entries from simple_cnt / _gid (bit 1 measured 11 % slower: the select puts the table load's wait before the row stores)
 #endif
+#ifndef CS_DDZ_CLEAN
+#define CS_DDZ_CLEAN 1   // zero only the dwords a step wrote, after its row is out (full zeroing when the list wrapped)
+#endif
 constexpr int PMASK_WORDS = CS_DDZ_PAD ? (MASK_WORDS / 4 + HW - 1) / HW * HW * 4 : MASK_WORDS;
 struct alignas(16) PairLds {
     uint32_t mask[PMASK_WORDS];                      // the shifted image (see above)
@@ -1303,14 +1306,15 @@ __global__ __launch_bounds__(PBLOCK, CS_DDZ_PAIR_MINW) void k_rollout2(uint32_t*
     }
     const uint64_t genv = env_base + (uint64_t)env;
     uint32_t rr_lane = 0;
+    bool dirty = true;   // CS_DDZ_CLEAN: the half's image holds bits the previous step did not clean
     for (int t = 0; t < T; t++) {
         const int64_t row = (int64_t)t * n + env;
-        {   // zero the mask image of both envs: 224 uint4 each, 32 lanes per env
+        if (CS_DDZ_CLEAN == 0 || __ballot(dirty)) {   // zero the mask image of both envs: 224 uint4 each, 32 lanes per env
             uint4* z = (uint4*)L.mask;
 #pragma unroll
             for (int j = 0; j < (PMASK_WORDS / 4 + HW - 1) / HW; j++) {
                 const int q = j * HW + hl;
-                if (CS_DDZ_PAD || q < PMASK_WORDS / 4) z[q] = make_uint4(0, 0, 0, 0);
+                if ((CS_DDZ_PAD || q < PMASK_WORDS / 4) && (CS_DDZ_CLEAN == 0 || dirty)) z[q] = make_uint4(0, 0, 0, 0);
             }
         }
         wave_sync_lds();
@@ -1334,6 +1338,18 @@ __global__ __launch_bounds__(PBLOCK, CS_DDZ_PAIR_MINW) void k_rollout2(uint32_t*
         wave_sync_lds();
         write_rows2(L, valid && !(CS_PROF_DDZ & 2) ? (uint8_t*)out.obs + row * OBS : nullptr,
                     valid && !(CS_PROF_DDZ & 1) ? (uint8_t*)out.legal + row * LB : nullptr, lane);
+        if constexpr (CS_DDZ_CLEAN != 0) {
+            // clean after the row is out: zero the dwords this step wrote (all listed unless the list ring wrapped)
+            // and the pass byte, instead of the whole image at the next step
+            dirty = lg.nl > (uint32_t)LIST_RING || (kfl & 2) != 0;   // kernel flag bit 1: A/B only
+            wave_sync_lds();
+#pragma unroll
+            for (int j = 0; j < LIST_RING / HW; j++) {
+                const uint32_t k = (uint32_t)(j * HW + hl);
+                if (!dirty && k < lg.nl) put_mask(L, L.lst[k], lmis, 0u);
+            }
+            if (hl == 0) ((uint8_t*)L.mask)[16u + lmis + PASS / 8] = 0;
+        }
         const uint32_t p = e.cur;
         if (valid) e.apply_with(a, ca, ga, hl);
         const bool done = valid && e.over();
