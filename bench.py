@@ -177,11 +177,16 @@ def main():
                     help='N>1: trajectory exchange timed after the main loop: every shard into rank 0 ("gather"), '
                          'all-gathered into every rank (BASELINE config 5, "allgather"), or both (default)')
     ap.add_argument('--gather-steps', type=int, default=5)
+    ap.add_argument('--recv-budget-gb', type=float, default=32.0,
+                    help='N>1: receive-buffer budget per GPU of the exchange (GiB); the trajectory moves in T-slices '
+                         'that fit it (rlcard_amd/shard.py exchange_traj)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-philox', dest='philox', action='store_false',
                     help='skip the CS_RNG_PHILOX phase (reported under "rng_philox")')
     ap.add_argument('--no-precondition', dest='precondition', action='store_false',
                     help='time from freshly seeded streams (optimistic: no MT block refills yet)')
+    ap.add_argument('--no-device-state', dest='device_state', action='store_false',
+                    help='skip the amd-smi / HIP attribute sample of the box (reported under "device")')
     args = ap.parse_args()
 
     import torch
@@ -228,8 +233,29 @@ def main():
         steps = int(min(4000, max(20, math.ceil(TIMED_TARGET_S / max(per, 1e-6)))))
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    dev_state, pw = {}, None
+    if rank == 0 and args.device_state:
+        # the box's state while the timed launches run (boxes run the same kernel at 3.5 or
+        # 4.3 ms): HIP attributes + amd-smi's clocks / partition modes (a host thread), and the power window --
+        # average power, package-power-limit (PPT) residency, XCD clocks -- from in-process gpu_metrics reads
+        import threading
+        from tools.device_state import device_state, PowerWindow
+        pw = PowerWindow(local)
+
+        stop_sampling = threading.Event()
+
+        def sample():
+            t_state = time.perf_counter() + 0.5
+            while not stop_sampling.wait(0.1):
+                pw.mid()
+                if not dev_state and time.perf_counter() >= t_state:
+                    dev_state.update(device_state(local))
+        sampler = threading.Thread(target=sample, daemon=True)
     barrier()
     torch.cuda.synchronize()
+    if pw is not None:
+        pw.start()
+        sampler.start()
     t0 = time.perf_counter()
     for k in range(steps):
         ev[k][0].record(stream)
@@ -237,9 +263,15 @@ def main():
         ev[k][1].record(stream)
         t_launch += 1
     torch.cuda.synchronize()
+    power = None
+    if pw is not None:
+        power = pw.stop()
+        stop_sampling.set()
     barrier()
     elapsed = rank_max(time.perf_counter() - t0, dev)
     kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    if rank == 0 and args.device_state:
+        sampler.join(timeout=60)   # the amd-smi query may outlast a short timed region
 
     gather_info = {}
     if world > 1 and args.gather != 'none':
@@ -249,7 +281,8 @@ def main():
                 nonlocal t_launch
                 env.rollout(T, policy_seed=5, t0=t_launch * T, out=traj)
                 t_launch += 1
-            info, gathered = time_exchange(produce, traj, mode, args.gather_steps, N, T, torch.cuda.synchronize, dev)
+            info, gathered = time_exchange(produce, traj, mode, args.gather_steps, N, T, torch.cuda.synchronize, dev,
+                                            budget_bytes=int(args.recv_budget_gb * (1 << 30)))
             gather_info['allgather' if mode == 'all' else 'gather'] = info
             del gathered
             torch.cuda.empty_cache()
@@ -319,6 +352,14 @@ def main():
             else:
                 line['roofline']['traffic'] = tr['bytes_per_launch']
                 line['roofline']['traffic_source'] = tr['source']
+        if dev_state or power:
+            smi = dev_state.get('smi') or {}
+            keep = ('bus', 'gfx_0_mhz', 'gfx_0_max_mhz', 'mem_0_mhz', 'fclk_0_mhz', 'power_w', 'power_cap_static',
+                    'temp_hotspot', 'temp_mem', 'driver')
+            line['device'] = dict(name=dev_state.get('name'), arch=dev_state.get('arch'), hip=dev_state.get('hip'),
+                                  smi={k: smi.get(k) for k in keep},
+                                  partition=(smi.get('partition') or {}).get('current_partition'),
+                                  timed_window=power)
         line.update(gather_info)
         if philox_info is not None:
             line['rng_philox'] = philox_info

@@ -9,6 +9,9 @@ consumer wants the trajectory shards in one place:
   buffers; RCCL over xGMI with the nccl backend). xGMI is point-to-point, so rank dst receives the 7 shards over its
   7 links at once, and no other rank holds world x the trajectory (gather to the consumer).
 * gather_traj(...): all-gather into every rank (world x the trajectory per GPU; for consumers on every rank).
+* exchange_traj(...): either exchange in T-slices through receive buffers of a stated budget (default 32 GiB per
+  GPU, checked before allocating), each slice handed to a consumer callback and optionally verified; this is what
+  bench.py times (config 5's all-gather would otherwise need 8 x 12.9 GB of receive buffers on every GPU).
 
 Timing across ranks (bench.py) goes through rank_max / whole_job_rate, so the aggregation is the one the gloo
 world-size-2 test checks.
@@ -17,7 +20,8 @@ import torch
 import torch.distributed as dist
 
 __all__ = ['shard_range', 'ShardedVecEnv', 'gather_traj', 'gather_traj_to', 'new_gathered', 'rank_max',
-           'whole_job_rate', 'traj_bytes', 'time_exchange', 'shard_digest', 'verify_gathered']
+           'whole_job_rate', 'traj_bytes', 'time_exchange', 'shard_digest', 'verify_gathered', 'exchange_traj',
+           'exchange_chunk_steps', 'RecvBuffers', 'DEFAULT_RECV_BUDGET']
 
 
 def shard_range(envs_per_rank, rank):
@@ -81,20 +85,31 @@ def gather_traj_to(traj, out, dst=0, group=None):
     return out if rank == dst else None
 
 
+_DIGEST_PIECE = 1 << 28   # bytes per aligned piece of shard_digest (a multiple of its 4 KiB blocks)
+
+
+def _block_sums(v):
+    """Wrapping int64 sums of a flat uint8 tensor's 4 KiB blocks (the last one zero-padded). Pieces that start off an
+    8-byte boundary (a slice of a gathered buffer whose shard size is not a multiple of 8) or end mid-block are copied
+    into an aligned zero-padded buffer first, so the int64 view is always legal."""
+    out = []
+    for s in range(0, v.numel(), _DIGEST_PIECE):
+        seg = v[s:s + _DIGEST_PIECE]
+        if seg.data_ptr() % 8 or seg.numel() % 4096:
+            b = torch.zeros((seg.numel() + 4095) // 4096 * 4096, dtype=torch.uint8, device=seg.device)
+            b[:seg.numel()] = seg
+            seg = b
+        out.append(seg.view(torch.int64).view(-1, 512).sum(dim=1))
+    return out
+
+
 def shard_digest(traj):
     """A position-sensitive fingerprint of a trajectory shard, computed where it lives: per tensor (sorted keys), the
     wrapping int64 sums of its bytes in 4 KiB blocks (the last block zero-padded). Equal digests on sender and receiver
     mean the slice arrived intact and in its place."""
     parts = []
     for k in sorted(traj):
-        v = traj[k].contiguous().view(-1).view(torch.uint8)
-        main = v.numel() // 4096 * 4096
-        if main:
-            parts.append(v[:main].view(torch.int64).view(-1, 512).sum(dim=1))
-        if v.numel() > main:
-            tail = torch.zeros(4096, dtype=torch.uint8, device=v.device)
-            tail[:v.numel() - main] = v[main:]
-            parts.append(tail.view(torch.int64).sum().reshape(1))
+        parts += _block_sums(traj[k].contiguous().view(-1).view(torch.uint8))
     return torch.cat(parts)
 
 
@@ -115,6 +130,95 @@ def verify_gathered(traj, gathered, group=None):
     return bool(flag.item())
 
 
+# -- bounded exchange: T-slices through fixed receive buffers ----------------------------------------------------------
+
+DEFAULT_RECV_BUDGET = 32 << 30   # receive-buffer bytes per GPU (BASELINE config 5 all-gather: 8 x 12.9 GB otherwise)
+
+
+def _steps(traj):
+    T = {int(v.shape[0]) for v in traj.values()}
+    if len(T) != 1:
+        raise ValueError('trajectory tensors disagree on T: %s' % sorted(T))
+    return T.pop()
+
+
+def exchange_chunk_steps(traj, world, budget_bytes=DEFAULT_RECV_BUDGET):
+    """T-rows per exchanged slice so that a receiver's buffers, world x rows x (bytes of one step of every tensor),
+    stay within budget_bytes. Every rank computes the same value from its own shard (shards have equal shapes).
+    Raises ValueError when not even one step fits."""
+    T = _steps(traj)
+    row = traj_bytes(traj) // max(T, 1)
+    tc = min(T, int(budget_bytes) // max(1, world * row))
+    if tc < 1:
+        raise ValueError('receive budget %d B cannot hold one step of %d shards (%d B)' % (budget_bytes, world,
+                                                                                          world * row))
+    return tc
+
+
+class RecvBuffers:
+    """Receive buffers for chunk_steps T-rows of `world` shards: one flat allocation per tensor, viewed for a slice
+    of n <= chunk_steps rows as a contiguous [world, n, ...] (what all_gather_into_tensor and the p2p receives
+    need). The size is checked against the budget and, on a GPU, the free device memory before allocating."""
+
+    def __init__(self, traj, world, chunk_steps, budget_bytes=DEFAULT_RECV_BUDGET):
+        self.world, self.chunk_steps = int(world), int(chunk_steps)
+        self.tail = {k: tuple(v.shape[1:]) for k, v in traj.items()}
+        per = {k: self.world * self.chunk_steps * v[0].numel() for k, v in traj.items()}
+        self.nbytes = sum(per[k] * traj[k].element_size() for k in traj)
+        if self.nbytes > budget_bytes:
+            raise ValueError('receive buffers of %d B exceed the budget of %d B' % (self.nbytes, budget_bytes))
+        dev = next(iter(traj.values())).device
+        if dev.type == 'cuda':
+            free, _ = torch.cuda.mem_get_info(dev)
+            if self.nbytes > free:
+                raise MemoryError('receive buffers of %d B exceed the %d B free on %s' % (self.nbytes, free, dev))
+        self.flat = {k: torch.empty(per[k], dtype=traj[k].dtype, device=dev) for k in traj}
+
+    def view(self, n):
+        """{key: [world, n, ...]} over the leading part of each flat buffer."""
+        return {k: f[:self.world * n * _numel(self.tail[k])].view((self.world, n) + self.tail[k])
+                for k, f in self.flat.items()}
+
+
+def _numel(shape):
+    m = 1
+    for d in shape:
+        m *= int(d)
+    return m
+
+
+def exchange_traj(traj, mode, recv=None, chunk_steps=None, dst=0, consume=None, verify=False, group=None,
+                  budget_bytes=DEFAULT_RECV_BUDGET):
+    """The trajectory exchange in T-slices of chunk_steps rows: for each slice [t0, t1) every shard's rows go to rank
+    dst (mode 'rank0') or to every rank (mode 'all') into `recv` (RecvBuffers, reused for every slice; allocated here
+    when None on a receiving rank), then consume(t0, t1, views) runs on the receiving ranks with views[k] =
+    [world, t1 - t0, N, ...] (rank-major: views[k][r] = global envs [r*N, (r+1)*N) at steps t0..t1-1). With
+    verify=True each slice is then checked against its senders' shard_digest (after consume, so whatever happened to
+    the slice before it was consumed is covered). -> (verified: bool or None, recv)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    T = _steps(traj)
+    if chunk_steps is None:
+        chunk_steps = recv.chunk_steps if recv is not None else exchange_chunk_steps(traj, world, budget_bytes)
+    receiving = mode == 'all' or rank == dst
+    if receiving and recv is None:
+        recv = RecvBuffers(traj, world, chunk_steps, budget_bytes)
+    ok = True
+    for t0 in range(0, T, chunk_steps):
+        t1 = min(T, t0 + chunk_steps)
+        piece = {k: v[t0:t1] for k, v in traj.items()}
+        views = recv.view(t1 - t0) if receiving else None
+        if mode == 'all':
+            gather_traj(piece, views, group)
+        else:
+            gather_traj_to(piece, views, dst, group)
+        if receiving and consume is not None:
+            consume(t0, t1, views)
+        if verify:
+            ok = verify_gathered(piece, views, group) and ok
+    return (ok if verify else None), recv
+
+
 def rank_max(x, device=None, group=None):
     """max over ranks of a host float (a per-rank elapsed time); x itself with one rank."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
@@ -129,13 +233,16 @@ def whole_job_rate(envs_per_rank, steps_per_launch, launches, elapsed_s, world):
     return world * int(envs_per_rank) * int(steps_per_launch) * int(launches) / float(elapsed_s)
 
 
-def time_exchange(produce, traj, mode, steps, envs_per_rank, steps_per_launch, sync=None, device=None):
-    """bench.py's N > 1 exchange phase: `steps` x (produce() refills traj, then the exchange: mode 'rank0' =
-    gather_traj_to rank 0, 'all' = gather_traj into every rank), bracketed by sync() + barrier, timed as the max
-    over ranks. -> (info dict, gathered buffers on the ranks that hold them, else None)."""
+def time_exchange(produce, traj, mode, steps, envs_per_rank, steps_per_launch, sync=None, device=None,
+                  budget_bytes=DEFAULT_RECV_BUDGET):
+    """bench.py's N > 1 exchange phase: `steps` x (produce() refills traj, then the exchange: mode 'rank0' = every
+    shard into rank 0, 'all' = into every rank; exchange_traj in T-slices whose receive buffers fit budget_bytes per
+    GPU), bracketed by sync() + barrier, timed as the max over ranks. -> (info dict, the receive buffers' view of the
+    last slice on the ranks that hold them, else None)."""
     world = dist.get_world_size()
     rank = dist.get_rank()
-    gathered = new_gathered(traj, world) if (mode == 'all' or rank == 0) else None
+    chunk = exchange_chunk_steps(traj, world, budget_bytes)
+    recv = RecvBuffers(traj, world, chunk, budget_bytes) if (mode == 'all' or rank == 0) else None
     sync = sync or (lambda: None)
     sync()
     dist.barrier()
@@ -143,21 +250,21 @@ def time_exchange(produce, traj, mode, steps, envs_per_rank, steps_per_launch, s
     t0 = time.perf_counter()
     for _ in range(steps):
         produce()
-        if mode == 'all':
-            gather_traj(traj, gathered)
-        else:
-            gather_traj_to(traj, gathered, dst=0)
+        exchange_traj(traj, mode, recv, chunk)
     sync()
     dist.barrier()
     el = rank_max(time.perf_counter() - t0, device)
+    T = _steps(traj)
     info = dict(mode=mode, collective='RCCL %s over xGMI' % (
                     'all_gather_into_tensor' if mode == 'all' else 'send/recv into rank 0'),
                 steps=steps, ms_per_step=1e3 * el / steps,
                 value=whole_job_rate(envs_per_rank, steps_per_launch, steps, el, world),
-                bytes_per_rank_per_step=traj_bytes(traj))
-    # untimed: the last exchange's slices checked against their senders' digests (shard_digest)
-    info['verified'] = verify_gathered(traj, gathered)
-    return info, gathered
+                bytes_per_rank_per_step=traj_bytes(traj), chunk_steps=chunk, chunks=-(-T // chunk),
+                recv_buffer_bytes=None if recv is None else recv.nbytes, recv_budget_bytes=int(budget_bytes))
+    # untimed: one more exchange of the last trajectory, every slice checked against its senders' digests
+    info['verified'], _ = exchange_traj(traj, mode, recv, chunk, verify=True)
+    last = T - (T - 1) // chunk * chunk
+    return info, (None if recv is None else recv.view(last))
 
 
 class ShardedVecEnv:

@@ -213,24 +213,36 @@ class VecEnv:
         games holds CS_RING_SLOTS blocks (rlcard_amd/csrc/cs_ring.h), doudizhu's word layout 2."""
         return int(self.info.rng_period)
 
+    def _rng_geometry(self):
+        """'words': doudizhu's two-block word window, or the Blackjack shoe's word stream (rng_period 624: one twist
+        per 624 draws); 'ring': the byte ring of the other lane-per-env games (rng_period = CS_RING_SLOTS x 624)."""
+        if self.env_id == 'doudizhu':
+            return 'ddz'
+        return 'words' if self.rng_period == 624 else 'ring'
+
     @property
     def rng_first_refill(self):
-        """Draws before the first refill, worst case over the envs (rng_first_refill_of): the lane games' seeding
-        generates 1 + e % (SLOTS - 1) ring blocks for env e (cs_ring.h seed_blocks) and a refill runs once the stream
-        is inside the latest, so env e first refills after (e % (SLOTS - 1)) x 624 draws, at most (SLOTS - 2) x 624;
-        doudizhu twists its next word block 624 draws in."""
-        return self.rng_period - 2 * 624 if self.env_id != 'doudizhu' else 624
+        """Draws before the first refill, worst case over the envs (rng_first_refill_of): the ring games' seeding
+        generates 1 + e % (SLOTS - 1) ring blocks for the handle-local env e (cs_ring.h seed_blocks) and a refill runs
+        once the stream is inside the latest, so env e first refills after (e % (SLOTS - 1)) x 624 draws, at most
+        (SLOTS - 2) x 624; doudizhu twists its next word block 624 draws in; the shoe's word stream twists at once."""
+        g = self._rng_geometry()
+        return {'ddz': 624, 'words': 0}.get(g, self.rng_period - 2 * 624)
 
     def rng_first_refill_of(self, env):
-        """Draws before env `env`'s first refill (global env id: env_base + env)."""
-        if self.env_id == 'doudizhu':
+        """Draws before env `env`'s first refill. `env` is the handle-local index (0..num_envs-1): cs_seed's
+        seed_blocks counts envs of the handle, not global ids, so shards of any env_base agree."""
+        g = self._rng_geometry()
+        if g == 'ddz':
             return 624
-        return ((self.env_base + int(env)) % (self.rng_period // 624 - 1)) * 624
+        if g == 'words':
+            return 0
+        return (int(env) % (self.rng_period // 624 - 1)) * 624
 
     @property
     def rng_per_refill(self):
-        """Draws between two refills: SLOTS - 1 blocks per ring refill; doudizhu one block."""
-        return self.rng_period - 624 if self.env_id != 'doudizhu' else 624
+        """Draws between two refills: SLOTS - 1 blocks per ring refill; doudizhu and the shoe's words one block."""
+        return self.rng_period - 624 if self._rng_geometry() == 'ring' else 624
 
     # heads-up hold'em games keep a deal queue after their 4 game words (rlcard_amd/csrc/cs_limit.h): deals drawn
     # ahead. 3..6-player hold'em has none (its judge may draw from the stream at a game's end, cs_holdem_n.h).

@@ -198,3 +198,81 @@ def test_nccl_world1_exchange_on_device_trajectories():
                 assert torch.equal(g[k][0], v), (mode, k)
     finally:
         dist.destroy_process_group()
+
+
+def _worker_chunked(rank, world, port, q):
+    """exchange_traj in T-slices through budget-bounded receive buffers (config 5's bounded all-gather), both modes:
+    the consumed slices reassemble the whole exchange; a slice altered before verification is caught; shard sizes
+    that are not a multiple of 8 bytes verify (digest of a misaligned slice); a budget below one step
+    raises before anything is allocated."""
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from rlcard_amd.shard import exchange_traj, exchange_chunk_steps, RecvBuffers, traj_bytes
+        T, N = 7, 5   # uint8 [T, N] rows: 5 B per step, odd shard sizes
+        g = torch.Generator().manual_seed(11 + rank)
+        traj = {'done': torch.randint(0, 255, (T, N), dtype=torch.uint8, generator=g),
+                'obs': torch.randint(0, 255, (T, N, 3), dtype=torch.uint8, generator=g),
+                'reward': torch.randn((T, N, 2), generator=g)}
+        row = traj_bytes(traj) // T
+        budget = world * 3 * row + 1
+        chunk = exchange_chunk_steps(traj, world, budget)
+        out = {}
+        for mode in ('rank0', 'all'):
+            got = []
+
+            def consume(t0, t1, views):
+                got.append((t0, t1, {k: v.clone() for k, v in views.items()}))
+            ok, recv = exchange_traj(traj, mode, consume=consume, verify=True, budget_bytes=budget)
+            out[mode] = (ok, [(a, b) for a, b, _ in got],
+                         None if not got else {k: torch.cat([v[k] for _, _, v in got], 1).numpy() for k in traj},
+                         None if recv is None else recv.nbytes)
+
+        def tamper(t0, t1, views):
+            if t0 == 3:
+                views['obs'][1 - rank, 0, 4, 2] ^= 1
+        bad, _ = exchange_traj(traj, 'all', consume=tamper, verify=True, budget_bytes=budget)
+        try:
+            RecvBuffers(traj, world, 1, budget_bytes=world * row - 1)
+            small = 'no error'
+        except ValueError:
+            small = 'ValueError'
+        try:
+            exchange_chunk_steps(traj, world, world * row - 1)
+            small2 = 'no error'
+        except ValueError:
+            small2 = 'ValueError'
+        q.put((rank, chunk, budget, out, bad, small, small2, {k: v.numpy() for k, v in traj.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_chunked_exchange_within_budget():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_chunked, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r[0]: r[1:] for r in [q.get(timeout=240) for _ in range(2)]}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    shards = [res[r][-1] for r in (0, 1)]
+    for r in (0, 1):
+        chunk, budget, out, bad, small, small2, _ = res[r]
+        assert chunk == 3
+        assert not bad, 'a slice altered before verification fails on every rank'
+        assert small == 'ValueError' and small2 == 'ValueError'
+        for mode in ('rank0', 'all'):
+            ok, spans, got, nbytes = out[mode]
+            assert ok
+            if mode == 'rank0' and r == 1:
+                assert spans == [] and got is None and nbytes is None, 'a sender holds no receive buffers'
+                continue
+            assert spans == [(0, 3), (3, 6), (6, 7)]
+            assert nbytes <= budget
+            for k in shards[0]:
+                for s in (0, 1):
+                    assert np.array_equal(got[k][s], shards[s][k]), (mode, k, s)

@@ -12,6 +12,8 @@
 #   profile:GAME[:ARGS...]    kernel trace + stats, then FETCH_SIZE and WRITE_SIZE passes over bench.py
 #   ab:GAME:N:T:F1[:F2...]    tools/ab_rollout.py kernel-flag A/B (AB_PLAYERS / AB_WARM from the env)
 #   abl:GAME:N:T:LIB1[:LIB2]  the same rollout timed with several library builds (CARDSIM_LIB), interleaved runs
+#   devstate / listctr        device state (tools/device_state.py), rocprofv3 -L
+#   pmc:GAME:N:T:CTR...       one PMC pass over tools/ab_rollout.py
 #   ceiling                   plain read / write streams and torch fill_ on this box (tools/calib.py --ceiling)
 set -o pipefail
 export TMPDIR=/tmp
@@ -85,6 +87,16 @@ for step in "$@"; do
         done
       done
       cat "$O/abl_$g.log" ;;
+    devstate)   # the box's device state (HIP attributes + raw amd-smi metric / static / partition JSON)
+      run 120 "$O/devstate.json" python3 tools/device_state.py --full
+      head -c 1500 "$O/devstate.json"; echo ;;
+    listctr)    # the PMC counters rocprofv3 offers on this box
+      run 120 "$O/counters_avail.txt" rocprofv3 -L
+      grep -i -c "" "$O/counters_avail.txt" ;;
+    pmc)        # pmc:GAME:N:T:CTR1[:CTR2..]  one PMC pass (caller keeps within the per-block limits)
+      g=${a[1]}; n=${a[2]}; t=${a[3]}; d=$O/pmc_${g}_$(echo "${a[@]:4}" | tr ' ' '_' | cut -c1-60); mkdir -p "$d"
+      run 120 "$d/run.log" rocprofv3 --pmc ${a[@]:4} --output-format csv -d "$d/p" -o p -- python3 tools/ab_rollout.py "$g" "$n" "$t" 0
+      python3 tools/pmc_summary.py "$d" > "$d/summary.txt" 2>&1; grep -A 12 k_rollout "$d/summary.txt" | head -30 ;;
     ceiling)
       run 300 "$O/ceiling.json" python3 tools/calib.py --ceiling
       cat "$O/ceiling.json" ;;
