@@ -198,6 +198,7 @@ class Env(object):
         self._last = out
         if was_over:        # lazy auto-reset: the engine dealt a new game instead (include/cardsim.h cs_step)
             self._payoffs = None
+            self._history = []   # a new game: nothing to step back into (the host bookkeeping restarts with it)
             self._after_deal()
         else:
             self._after_step(player, decoded, before)

@@ -160,6 +160,28 @@ def test_step_back_restores_the_game(game, name):
                 assert snap(state, player) == seen[j + 1]
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize('game,name', GAMES)
+def test_step_on_a_finished_game_starts_a_new_one_without_history(game, name):
+    """A step on a finished game is the engine's lazy auto-reset (include/cardsim.h cs_step): a new game with an empty
+    step_back history, so step_back returns False instead of restoring the old game into the new deal's host
+    bookkeeping (DouDizhu's trace / No-limit's type stack raised IndexError there)."""
+    env = rlcard_amd.make(game, config={'seed': 3, 'allow_step_back': True})
+    rng = np.random.RandomState(2)
+    state, _ = env.reset()
+    while not env.is_over():
+        state, _ = env.step(int(rng.choice(list(state['legal_actions'].keys()))))
+    state, player = env.step(0)   # ignored: the engine deals the next game
+    assert not env.is_over()
+    assert env.step_back() is False
+    a = int(rng.choice(list(state['legal_actions'].keys())))
+    s1, p1 = env.step(a)
+    s0, p0 = env.step_back()
+    assert p0 == player and s0['obs'].tobytes() == state['obs'].tobytes()
+    assert list(s0['legal_actions']) == list(state['legal_actions'])
+    assert env.step_back() is False
+
+
 def test_step_back_is_off_by_default():
     import torch as _t
     if not _t.cuda.is_available():
