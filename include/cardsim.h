@@ -241,8 +241,18 @@ int cs_set_step_record(cs_handle* h, int64_t env, uint32_t* words, uint32_t* seq
 
 /* Overwrite the packed state words of env `env` from a HOST buffer taken by cs_get_env_state: Env.step_back
  * (envs/env.py:88-108) restores the game from its history. The env's RNG stream is left where it is, as the
- * reference's np_random is not part of the restored history. Synchronous. */
+ * reference's history does not hold np_random for most games (Blackjack's does: cs_load_env_rng). Synchronous. */
 int cs_set_env_state(cs_handle* h, int64_t env, const uint32_t* host_words, int32_t nwords);
+
+/* An env's whole RNG stream (numpy RandomState: position word + MT19937 block words / byte ring) as *words u32, for
+ * the state a deep copy of the reference's RandomState holds. cs_copy_env_rng copies env `env`'s stream into dst,
+ * cs_load_env_rng writes it back from src (both DEVICE memory, asynchronous on `stream`). Blackjack's Game.step
+ * deep-copies the dealer -- its np_random included -- before every step and Game.step_back restores that copy
+ * (rlcard/games/blackjack/game.py:66-70, 125-135), so the reference's redraws after a step back replay the undone
+ * cards: rlcard_amd.make's Blackjack Env snapshots the stream with its history and loads it on step_back. */
+int cs_env_rng_words(cs_handle* h, int32_t* words);
+int cs_copy_env_rng(cs_handle* h, int64_t env, uint32_t* dst, void* stream);
+int cs_load_env_rng(cs_handle* h, int64_t env, const uint32_t* src, void* stream);
 
 /* Stream position (u32 draws consumed) bookkeeping word of env `env` (HOST out). Synchronous; for parity tests.
  * Hold'em envs: the position includes the draws of the queued deals (see cs_get_env_state). */

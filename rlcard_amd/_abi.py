@@ -51,7 +51,8 @@ class DmcBatch(C.Structure):
 # every symbol include/cardsim.h declares (tests check the library exports all of them)
 SYMBOLS = ('cs_game_info_get', 'cs_create', 'cs_destroy', 'cs_seed', 'cs_reset', 'cs_step', 'cs_observe',
            'cs_rollout', 'cs_transitions', 'cs_legal_lists', 'cs_action_features', 'cs_get_env_state',
-           'cs_set_env_state', 'cs_copy_env_state', 'cs_set_step_record', 'cs_get_rng_ctl', 'cs_cfr_train', 'cs_debug_holdem_rank7', 'cs_debug_ddz_legal',
+           'cs_set_env_state', 'cs_copy_env_state', 'cs_set_step_record', 'cs_env_rng_words', 'cs_copy_env_rng',
+           'cs_load_env_rng', 'cs_get_rng_ctl', 'cs_cfr_train', 'cs_debug_holdem_rank7', 'cs_debug_ddz_legal',
            'cs_debug_set_serial_refill', 'cs_debug_set_kernel_flags',
            'cs_dmc_create', 'cs_dmc_destroy', 'cs_dmc_fill', 'cs_dmc_gather', 'cs_dmc_status', 'cs_dmc_layer1',
            'cs_dmc_select', 'cs_last_error', 'cs_version')
@@ -88,6 +89,9 @@ def lib():
     L.cs_set_env_state.argtypes = [vp, i64, vp, i32]
     L.cs_copy_env_state.argtypes = [vp, i64, vp, vp]
     L.cs_set_step_record.argtypes = [vp, i64, vp, vp]
+    L.cs_env_rng_words.argtypes = [vp, vp]
+    L.cs_copy_env_rng.argtypes = [vp, i64, vp, vp]
+    L.cs_load_env_rng.argtypes = [vp, i64, vp, vp]
     L.cs_get_rng_ctl.argtypes = [vp, i64, vp]
     L.cs_cfr_train.argtypes = [vp, i32, i64, vp, vp, vp, vp, vp]
     L.cs_debug_holdem_rank7.argtypes = [vp, i64, vp, vp]

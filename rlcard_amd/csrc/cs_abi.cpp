@@ -455,6 +455,46 @@ int cs_set_env_state(cs_handle* h, int64_t env, const uint32_t* host_words, int3
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_set_env_state");
 }
 
+// the env's mt footprint (u32) and layout, as cs_create allocated it
+static void rng_layout(const cs_handle* h, int32_t* mtw, int32_t* column)
+{
+    const int32_t p = h->info.rng_period;
+    *mtw = p == 2 * 624 ? 2 * 624 : p == 624 ? 624 : (int32_t)cs::RING_ENV_WORDS_HOST;
+    *column = p == 624 ? 1 : 0;   // Blackjack shoes: word k of env e at mt[k * n + e]
+}
+
+int cs_env_rng_words(cs_handle* h, int32_t* words)
+{
+    if (!h || !words) return fail(CS_E_INVALID, "null argument");
+    int32_t mtw, column;
+    rng_layout(h, &mtw, &column);
+    *words = 1 + mtw;
+    return CS_OK;
+}
+
+static int rng_copy(cs_handle* h, int64_t env, uint32_t* buf, int32_t load, void* stream, const char* what)
+{
+    if (!h || !buf) return fail(CS_E_INVALID, "null argument");
+    if (env < 0 || env >= h->b.n) return fail(CS_E_INVALID, "bad env");
+    int r = set_device(h);
+    if (r != CS_OK) return r;
+    int32_t mtw, column;
+    rng_layout(h, &mtw, &column);
+    const uint32_t clear = h->b.sbuf ? (1u << 17) : 0u;   // restored streams restage from the ring
+    hipError_t e = cs::launch_rng_copy(h->b, env, mtw, column, clear, buf, load, (hipStream_t)stream);
+    return e == hipSuccess ? CS_OK : fail_hip(e, what);
+}
+
+int cs_copy_env_rng(cs_handle* h, int64_t env, uint32_t* dst, void* stream)
+{
+    return rng_copy(h, env, dst, 0, stream, "cs_copy_env_rng");
+}
+
+int cs_load_env_rng(cs_handle* h, int64_t env, const uint32_t* src, void* stream)
+{
+    return rng_copy(h, env, const_cast<uint32_t*>(src), 1, stream, "cs_load_env_rng");
+}
+
 int cs_get_rng_ctl(cs_handle* h, int64_t env, uint32_t* host_ctl)
 {
     if (!h || !host_ctl) return fail(CS_E_INVALID, "null argument");

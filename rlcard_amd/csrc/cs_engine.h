@@ -159,6 +159,8 @@ hipError_t launch_legal_lists(const Buffers& b, int32_t lb, const uint8_t* legal
                               int64_t* offsets, int32_t* ids, void** tmp, size_t* tmp_bytes, hipStream_t s);
 hipError_t launch_onehot(const int32_t* ids, int64_t count, int32_t na, uint8_t* out, hipStream_t s);
 hipError_t launch_copy_state(const Buffers& b, int64_t env, int32_t sw, uint32_t* dst, hipStream_t s);
+hipError_t launch_rng_copy(const Buffers& b, int64_t env, int32_t mtw, int32_t column, uint32_t clear_mask,
+                           uint32_t* buf, int32_t load, hipStream_t s);   // cs_traj.hip
 hipError_t launch_debug_rank7(const int8_t* cards, int64_t n, uint32_t* values, hipStream_t s);   // cs_kernels.hip
 
 namespace ddz {   // cs_doudizhu.hip (seeding goes through the shared k_seed)

@@ -237,6 +237,33 @@ hipError_t launch_copy_state(const Buffers& b, int64_t env, int32_t sw, uint32_t
     return hipGetLastError();
 }
 
+// one env's RNG stream (cs_copy_env_rng / cs_load_env_rng): buf = ctl word, then the env's mt words (env-major at
+// mt + env * mtw, or a column mt[k * n + env] for the Blackjack shoe). load = 1 writes the env from buf; clear_mask
+// then drops ctl bits (the rollout's "staged rows valid" bit: the restored position restages from the ring).
+__global__ __launch_bounds__(TBLOCK) void k_rng_copy(uint32_t* __restrict__ mt, uint32_t* __restrict__ ctl, int64_t n,
+                                                     int64_t env, int mtw, int column, uint32_t clear_mask,
+                                                     uint32_t* __restrict__ buf, int load)
+{
+    for (int k = (int)threadIdx.x; k <= mtw; k += TBLOCK) {
+        if (k == 0) {
+            if (load) ctl[env] = buf[0] & ~clear_mask;
+            else buf[0] = ctl[env];
+            continue;
+        }
+        uint32_t* w = column ? mt + (int64_t)(k - 1) * n + env : mt + env * mtw + (k - 1);
+        if (load) *w = buf[k];
+        else buf[k] = *w;
+    }
+}
+
+hipError_t launch_rng_copy(const Buffers& b, int64_t env, int32_t mtw, int32_t column, uint32_t clear_mask,
+                           uint32_t* buf, int32_t load, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_rng_copy, dim3(1), dim3(TBLOCK), 0, s, b.mt, b.ctl, b.n, env, mtw, column, clear_mask, buf,
+                       load);
+    return hipGetLastError();
+}
+
 hipError_t launch_onehot(const int32_t* ids, int64_t count, int32_t na, uint8_t* out, hipStream_t s)
 {
     const int64_t total = count * na;

@@ -117,9 +117,10 @@ class DoudizhuEnv(Env):
 
     def _decode_action(self, action_id):
         """An id outside the legal set: lowest solo when leading, pass when following (include/cardsim.h cs_step;
-        the reference would corrupt the hands)."""
+        the reference would corrupt the hands). A finished game has no legal ids: the engine ignores the action and
+        deals the next game (lazy auto-reset)."""
         legal = self._legal_ids(self._last)
-        if action_id in legal:
+        if action_id in legal or not legal:
             return ID_2_ACTION[action_id]
         if PASS_ID in legal:
             return 'pass'

@@ -170,6 +170,7 @@ class Env(object):
         return out
 
     def reset(self):
+        self._before_deal()
         out = self._call('reset')
         self.action_recorder = []
         self._payoffs = None
@@ -186,12 +187,14 @@ class Env(object):
             raise ValueError('action id %d out of range [0, %d)' % (a, self.num_actions))
         decoded = self._decode_action(a)
         if self.allow_step_back:
-            self._history.append((self._state_words(), dict(self._last), self._payoffs))
+            self._history.append((self._state_words(), dict(self._last), self._payoffs, self._snapshot_extra()))
         self.timestep += 1
         player = self.get_player_id()
         self.action_recorder.append((player, decoded))
         was_over = bool(self._last['done'])
         before = self._state_words()
+        if was_over:
+            self._before_deal()
         out = self._call('step', self._action_id(decoded))
         if out['done']:
             self._payoffs = out['reward']
@@ -207,18 +210,20 @@ class Env(object):
     def step_back(self):
         """env.py:88-108: restore the game as it was before the last step (the packed state words, written back
         with cs_set_env_state); False at the start of a game. Like the reference, whose history does not hold
-        np_random, the env's RNG stream is not rewound."""
+        np_random, the env's RNG stream is not rewound -- except for Blackjack, whose history holds the dealer's
+        RandomState (_snapshot_extra / _restore_extra)."""
         if not self.allow_step_back:
             raise Exception('Step back is off. To use step_back, please set allow_step_back=True in rlcard.make')
         if not self._history:
             return False
-        words, last, payoffs = self._history.pop()
+        words, last, payoffs, extra = self._history.pop()
         current = self._state_words()
         gw = self._vec.game_words
         if gw is not None:   # hold'em: the game words only; deals already drawn ahead stay queued
             words = list(words[:gw]) + self._vec.env_state_words(0)[gw:]
         words = self._step_back_words(list(words), current)
         self._vec.set_env_state_words(0, words)
+        self._restore_extra(extra)
         self._words = list(words)
         self._last, self._payoffs = last, payoffs
         self._after_step_back()
@@ -319,6 +324,17 @@ class Env(object):
         pass
 
     def _after_step_back(self):
+        pass
+
+    # device-side parts of the step_back history beyond the state words (Blackjack: the dealer's RandomState)
+    def _snapshot_extra(self):
+        return None
+
+    def _restore_extra(self, extra):
+        pass
+
+    def _before_deal(self):
+        """Called before the engine deals a new game (reset, or the lazy auto-reset of a step on a finished game)."""
         pass
 
     def _step_back_words(self, words, current):

@@ -24,6 +24,19 @@ class LeducholdemEnv(Env):
             return 'check' if 3 in legal else 'fold'
         return self.actions[action_id]
 
+    def _obs_of(self, obs_bytes, player_id):
+        """_extract_state (leducholdem.py:59-64) sets obs[sum(all_chips) - my_chips + 21]: with 3+ players the others'
+        chips can pass 14 and the index 36, where the reference raises IndexError -- after Game.step has advanced,
+        so is_over / get_payoffs / the next step see the new state. This Env raises the same error at the same point.
+        (The engine's batched rows hold the other slots -- hand, public card, my chips -- and no bit for the
+        out-of-range one: cs_holdem_n.h LeducN::observe.) Heads-up the index stays <= 35 (others' chips <= 14)."""
+        if self.num_players > 2:
+            f = self._fields()
+            k = sum(f['chips']) - f['chips'][player_id] + 21
+            if k >= 36:
+                raise IndexError('index %d is out of bounds for axis 0 with size 36' % k)
+        return obs_bytes.astype(np.float64)
+
     def _fields(self):
         w = self._state_words()
         if self.num_players > 2:   # cs_holdem_n.h LeducN: a word per player (hand:3 in:5), then pub:3 rc:2 ptr:3

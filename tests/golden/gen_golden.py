@@ -453,7 +453,10 @@ class RawStream:
         np.savez_compressed(path, **d)
 
 
-def drive_raw(rec, si, env_id, cfg, seed, games, sb_prob, pick):
+def drive_raw(rec, si, env_id, cfg, seed, games, sb_prob, pick, sb_after_over=0.0):
+    """sb_after_over > 0: a finished game is also stepped back with that probability (per check) and play goes on
+    from the restored state (Blackjack: Game.step_back puts the last actor's snapshot into the pointer's seat, which
+    is seat 0 after the dealer's turn, game.py:125-135)."""
     import random
     import rlcard
     env = rlcard.make(env_id, config=dict(cfg, seed=seed, allow_step_back=sb_prob > 0))
@@ -462,7 +465,13 @@ def drive_raw(rec, si, env_id, cfg, seed, games, sb_prob, pick):
         state, player = env.reset()
         rec.add(si, 0, -1, state, player, env)
         nsteps = 0
-        while not env.is_over():
+        while True:
+            if env.is_over():
+                if not (sb_after_over > 0 and rng.random() < sb_after_over):
+                    break
+                state, player = env.step_back()
+                rec.add(si, 2, -1, state, player, env)
+                continue
             if sb_prob > 0 and rng.random() < sb_prob:
                 r = env.step_back()
                 if r is not False:
@@ -500,15 +509,22 @@ def gen_raw():
                       ('blackjack', {}, 42, 25, 0.0, lambda rng, s, e: rng.randrange(2)),
                       ('blackjack', {'game_num_players': 3}, 5, 15, 0.0, lambda rng, s, e: rng.randrange(2)),
                       ('blackjack', {'game_num_players': 5, 'game_num_decks': 6}, 9, 8, 0.0,
-                       lambda rng, s, e: rng.randrange(2))],
+                       lambda rng, s, e: rng.randrange(2)),
+                      # step_back (game.py:66-70, 125-135): the dealer's RandomState rewinds with its deep copy, the
+                      # game's own stream does not (the next game deals from it); the snapshot goes to the current seat
+                      ('blackjack', {}, 3, 30, 0.35, lambda rng, s, e: rng.randrange(2), 0.5),
+                      ('blackjack', {'game_num_players': 3}, 7, 20, 0.35, lambda rng, s, e: rng.randrange(2), 0.5),
+                      ('blackjack', {'game_num_decks': 6}, 11, 20, 0.35, lambda rng, s, e: rng.randrange(2), 0.5),
+                      ('blackjack', {'game_num_players': 3, 'game_num_decks': 6}, 13, 15, 0.35,
+                       lambda rng, s, e: rng.randrange(2), 0.5)],
         'doudizhu': [('doudizhu', {}, 0, 2, 0.0, pick_legal), ('doudizhu', {}, 42, 1, 0.0, pick_legal),
                      ('doudizhu', {}, 1, 2, 0.25, pick_legal), ('doudizhu', {}, 12941, 2, 0.0, pick_legal)],
     }
     for name, streams in specs.items():
         rec = RawStream()
         meta = []
-        for si, (env_id, cfg, seed, games, sb, pick) in enumerate(streams):
-            drive_raw(rec, si, env_id, cfg, seed, games, sb, pick)
+        for si, (env_id, cfg, seed, games, sb, pick, *after) in enumerate(streams):
+            drive_raw(rec, si, env_id, cfg, seed, games, sb, pick, *after)
             meta.append({'env_id': env_id, 'config': cfg, 'seed': seed, 'games': games, 'step_back': sb > 0})
         rec.save(os.path.join(OUT, 'raw_%s.npz' % name), meta)
         print('raw_%s.npz: %d events (%d step_back)' % (name, len(rec.state), rec.cols['kind'].count(2)))

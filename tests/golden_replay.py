@@ -77,6 +77,8 @@ def replay(d, make_env, num_actions, check_final=True):
         if n >= 0:
             assert np.array_equal(got_obs[:n], exp_obs[:n]), ctx + ' obs\n%s\n%s' % (got_obs[:n], exp_obs[:n])
             assert not got_obs[n:].any(), ctx + ' obs padding'
+        else:   # Leduc's others'-chips slot is past 35: the row holds hand, [public,] my chips and nothing in 21..35
+            assert not got_obs[21:].any() and got_obs[:3].sum() == 1 and got_obs[6:21].sum() == 1, ctx + ' raised row'
         exp_legal = legal_bits_of(d, k, num_actions)
         got_legal = np.asarray(out['legal']).reshape(-1)
         assert np.array_equal(got_legal, exp_legal), ctx + ' legal %s vs %s' % (

@@ -128,11 +128,12 @@ def test_env_run_layout_and_types(game, name):
 @pytest.mark.gpu
 @pytest.mark.parametrize('game,name', GAMES)
 def test_step_back_restores_the_game(game, name):
-    """Env.step_back (env.py:88-108): the state before each step comes back exactly, and for Leduc and DouDizhu
-    replaying the same actions reproduces the same states. Not for Blackjack (its steps draw cards), nor for the two
-    Texas games, whose reference step_back leaves part of the game behind: limit hold'em keeps the undone steps' raise
-    history (game.py:167-168), no-limit's round reads a detached dealer's pot from then on (game.py:137-143, 219), so
-    raises after a step back can differ; tests/test_raw.py replays the reference's own streams through both."""
+    """Env.step_back (env.py:88-108): the state before each step comes back exactly, and for Leduc, DouDizhu and
+    Blackjack replaying the same actions reproduces the same states (Blackjack's history holds the dealer's
+    RandomState, games/blackjack/game.py:66-70, so the hits redraw the undone cards). Not for the two Texas games,
+    whose reference step_back leaves part of the game behind: limit hold'em keeps the undone steps' raise history
+    (game.py:167-168), no-limit's round reads a detached dealer's pot from then on (game.py:137-143, 219), so raises
+    after a step back can differ; tests/test_raw.py replays the reference's own streams through all of them."""
     env = rlcard_amd.make(game, config={'seed': 5, 'allow_step_back': True})
     rng = np.random.RandomState(1)
 
@@ -154,7 +155,7 @@ def test_step_back_restores_the_game(game, name):
             state, player = env.step_back()
             assert snap(state, player) == seen[j - 1] and not env.is_over()
         assert env.step_back() is False
-        if game in ('leduc-holdem', 'doudizhu'):
+        if game in ('leduc-holdem', 'doudizhu', 'blackjack'):
             for j, a in enumerate(acts):
                 state, player = env.step(a)
                 assert snap(state, player) == seen[j + 1]

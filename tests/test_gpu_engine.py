@@ -153,6 +153,68 @@ def test_rollout_matches_oracle(oracle, game, name, flags):
         assert v.rng_position(i) == ob.draws(i) % v.rng_period
 
 
+@pytest.mark.parametrize('flags', [0, 1, 2])
+def test_doudizhu_odd_counts(oracle, flags):
+    """The DouDizhu rollout gives each half-wave one env (k_rollout2, cs_doudizhu.hip), so an odd env count leaves the
+    last pair's second half empty (masked). The reference is per env (doudizhu/game.py:23-81), so every env must
+    come out as in any other batch: 257 envs -- reset, single steps, 3 chained rollouts and stream positions vs the
+    oracle; 65 537 envs (the bench size + 1) -- 3 launches of the bench's T = 64 compared on windows at the start, an
+    odd offset and the end (the half-empty pair). Flags 1 / 2 are the kernel variants of test_rollout_matches_oracle."""
+    n = 257
+    v = _vec('doudizhu', n, seed=11)
+    v.set_kernel_flags(flags)
+    ob = _oracle_batch(oracle, 'doudizhu', range(11, 11 + n))
+    exp = ob.reset()
+    _assert_same(_np(v.reset()), exp, 'reset')
+    rng = np.random.RandomState(4)
+    for t in range(6):
+        acts = np.zeros(n, np.int32)
+        for i in range(n):
+            ids = np.nonzero(np.unpackbits(exp['legal'][i], bitorder='little'))[0]
+            acts[i] = ids[rng.randint(len(ids))] if len(ids) else 0
+        exp = ob.step(acts)
+        _assert_same(_np(v.step(torch.from_numpy(acts).cuda())), exp, 'step %d' % t)
+    for c in range(3):
+        _assert_same(_np(v.rollout(48, policy_seed=13, t0=c * 48)), ob.rollout(48, 13, c * 48, 0), 'rollout %d' % c)
+    torch.cuda.synchronize()
+    for i in (0, 1, 128, 255, 256):
+        assert v.rng_position(i) == ob.draws(i) % v.rng_period, i
+    n, T, win = 65536 + 1, 64, 33
+    v = _vec('doudizhu', n, seed=42)
+    v.set_kernel_flags(flags)
+    v.reset()
+    out = v.new_traj_out(T)
+    starts = (0, n // 2 - 3, n - win)
+    obs = {s: _oracle_batch(oracle, 'doudizhu', range(42 + s, 42 + s + win)) for s in starts}
+    for s in starts:
+        obs[s].reset()
+    for c in range(3):
+        tr = v.rollout(T, policy_seed=5, t0=c * T, out=out)
+        for s in starts:
+            got = {k: x[:, s:s + win].cpu().numpy() for k, x in tr.items()}
+            _assert_same(got, obs[s].rollout(T, 5, c * T, s), 'n %d launch %d window %d' % (n, c, s))
+    for s in starts:
+        assert v.rng_position(s + win - 1) == obs[s].draws(win - 1) % v.rng_period
+
+
+def test_doudizhu_odd_count_past_mt_twists(oracle):
+    """65 DouDizhu envs (an odd count: the last wave holds one env in its first half) for 22 x 64 = 1 408 steps,
+    every env past its first word-window twist and the MT_WORDS wrap (test_gpu_refill's DouDizhu case, ragged)."""
+    n = 65
+    v = _vec('doudizhu', n, seed=9)
+    ob = _oracle_batch(oracle, 'doudizhu', range(9, 9 + n))
+    _assert_same(_np(v.reset()), ob.reset(), 'reset')
+    out = v.new_traj_out(64)
+    for c in range(22):
+        _assert_same(_np(v.rollout(64, policy_seed=2, t0=c * 64, out=out)), ob.rollout(64, 2, c * 64, 0),
+                     'launch %d' % c)
+    torch.cuda.synchronize()
+    d = np.array([ob.draws(i) for i in range(n)])
+    assert d.min() >= 1300, d.min()
+    for i in (0, 31, 32, 63, 64):
+        assert v.rng_position(i) == d[i] % v.rng_period, i
+
+
 @pytest.mark.parametrize('players,decks', [(2, 1), (4, 1), (1, 0), (3, 0)])
 def test_blackjack_configs_match_oracle(oracle, players, decks):
     """Blackjack with 2-4 players and the infinite deck (num_decks 0: a dealt card stays in the deck), step API and

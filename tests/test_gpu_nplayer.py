@@ -134,14 +134,20 @@ def test_nplayer_compat_env(game, players):
             assert len(raw['all_chips']) == players
 
 
-def test_leduc_nplayer_payoffs_exact_float64():
-    """N-player Leduc through rlcard_amd.make: Env.get_payoffs equals the reference's float64 payoffs exactly
-    (float(total) / #winners, leducholdem/judger.py:50-56, / big blind), unrounded, for every game of leduc_np.npz
-    (3..5 players, three-way splits included). The engine's reward rows are f32 (ABI); the compat Env rebuilds the
-    float64 values with the reference's operations."""
+def test_leduc_nplayer_payoffs_exact_float64_and_index_errors():
+    """N-player Leduc through rlcard_amd.make, every event of leduc_np.npz (3..5 players):
+    * Env.get_payoffs equals the reference's float64 payoffs exactly (float(total) / #winners,
+      leducholdem/judger.py:50-56, / big blind), unrounded. The engine's reward rows are f32 (ABI); the compat Env
+      rebuilds the float64 values with the reference's operations.
+    * Env.step / Env.get_state raise IndexError exactly where the reference's _extract_state did
+      (envs/leducholdem.py:63-64, the fixture's obs_len -1 events), after the game has advanced as the reference's
+      has; every other observation equals the fixture's."""
     import rlcard_amd
     d = gr.load('leduc_np')
-    checked = nonbinary = 0
+    fin_rows = {}
+    for j, g in enumerate(d['fin_game']):
+        fin_rows.setdefault(int(g), []).append(j)
+    checked = raised = fin_raised = 0
     env, cur = None, -1
     for k in range(len(d['ev_env'])):
         ei = int(d['ev_env'][k])
@@ -149,16 +155,30 @@ def test_leduc_nplayer_payoffs_exact_float64():
             env = rlcard_amd.make('leduc-holdem', config={'seed': int(d['seeds'][ei]),
                                                           'game_num_players': int(d['env_np'][ei])})
             cur = ei
+        n = int(d['ev_obs_len'][k])
         if d['ev_kind'][k] == 0:
-            env.reset()
-            continue
-        env.step(int(d['ev_act'][k]))
-        assert int(env.is_over()) == int(d['ev_done'][k])
-        if d['ev_done'][k]:
+            state, _ = env.reset()
+        elif n < 0:
+            with pytest.raises(IndexError):
+                env.step(int(d['ev_act'][k]))
+            raised += 1
+            state = None
+        else:
+            state, _ = env.step(int(d['ev_act'][k]))
+        if state is not None:
+            assert np.array_equal(state['obs'], d['ev_obs'][k][:36].astype(np.float64)), k
+        assert int(env.is_over()) == int(d['ev_done'][k]) and env.get_player_id() == int(d['ev_player'][k]), k
+        if d['ev_kind'][k] != 0 and d['ev_done'][k]:
             n = env.num_players
             got, exp = env.get_payoffs(), d['ev_payoff'][k][:n]
             assert got.dtype == np.float64 and np.array_equal(got, exp), (k, got, exp)
             checked += 1
-            nonbinary += int(np.any(exp * 2 != np.round(exp * 2)))   # split pots with an odd total
+            for p, j in enumerate(fin_rows[int(d['ev_game'][k])]):
+                if int(d['fin_obs_len'][j]) < 0:
+                    with pytest.raises(IndexError):
+                        env.get_state(p)
+                    fin_raised += 1
+                else:
+                    assert np.array_equal(env.get_state(p)['obs'], d['fin_obs'][j][:36].astype(np.float64)), (k, p)
     # a Leduc deck holds two cards per rank, so at most two players split: the values are multiples of 0.25
-    assert checked > 100, (checked, nonbinary)
+    assert checked > 100 and raised > 0 and fin_raised > 0, (checked, raised, fin_raised)

@@ -110,6 +110,70 @@ def test_full_size_after_precondition(oracle, game, win):
             assert v.rng_position(start + i) == d[i] % v.rng_period
 
 
+def test_config5_last_shard_full_size(oracle):
+    """BASELINE config 5's rank-7 shard on one GPU, exactly as bench.py runs it there: global env ids
+    7 * 2^20 .. 8 * 2^20 - 1 (seeds 42 + global id, the Philox policy counter on the global id), T = 256 after
+    bench.precondition_launches, one timed-shape launch compared with the oracle on three windows replayed from the
+    global ids; then the trajectory exchange of bench.py's N > 1 phase over RCCL at world size 1 in both modes (the
+    'all' mode through receive buffers bounded to ~1/3 of the shard, so the T-sliced path runs), every slice verified
+    against the shard digests. Reference: SURVEY 8(d) C5; rlcard/utils/seeding.py:33-113 (the high seeds' keys)."""
+    import torch.distributed as dist
+    import bench
+    from rlcard_amd.shard import ShardedVecEnv, time_exchange, traj_bytes
+    from test_shard import _free_port
+    game, rank = 'leduc-holdem', 7
+    g = bench.GAMES[game]
+    n, T = g['envs'], g['T']
+    base = rank * n
+    env = ShardedVecEnv(game, n, rank, seed=42, device=0)
+    assert env.env_base == base == 7340032
+    env.reset()
+    out = env.new_traj_out(T)
+    pre = bench.precondition_launches(game, T, env.vec)
+    for c in range(pre):
+        env.rollout(T, policy_seed=5, t0=c * T, out=out)
+    tr = env.rollout(T, policy_seed=5, t0=pre * T, out=out)
+    torch.cuda.synchronize()
+    win = 256
+    for start in (0, n // 2 + 17, n - win):
+        gid = base + start
+        ob = _oracle_batch(oracle, game, range(42 + gid, 42 + gid + win))
+        ob.reset()
+        for c in range(pre):
+            ob.rollout(T, 5, c * T, gid)
+        exp = ob.rollout(T, 5, pre * T, gid)
+        got = {k: x[:, start:start + win].cpu().numpy() for k, x in tr.items()}
+        _assert_same(got, exp, 'rank-7 window %d (global %d)' % (start, gid))
+        d = _draws(ob, win)
+        first = np.array([env.rng_first_refill_of(start + i) for i in range(win)])
+        assert (d >= first + 300).all(), 'window %d: an env has not refilled (%d)' % (start, (d - first).min())
+        for i in (0, win - 1):
+            assert env.rng_position(start + i) == d[i] % env.rng_period
+    snap = {k: v.clone() for k, v in out.items()}
+    dev = torch.device('cuda', 0)
+    dist.init_process_group('nccl', init_method='tcp://127.0.0.1:%d' % _free_port(), rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        t = [pre + 1]
+
+        def produce():
+            env.rollout(T, policy_seed=5, t0=t[0] * T, out=out)
+            t[0] += 1
+        for mode, budget in (('rank0', 32 << 30), ('all', traj_bytes(out) // 3)):
+            info, last = time_exchange(produce, out, mode, 1, n, T, torch.cuda.synchronize, dev, budget_bytes=budget)
+            assert info['verified'] and info['value'] > 0, info
+            assert info['recv_buffer_bytes'] <= budget
+            c = info['chunk_steps']
+            assert info['chunks'] == -(-T // c) and (mode == 'rank0' or info['chunks'] >= 3), info
+            lo = (T - 1) // c * c
+            for k, v in out.items():
+                assert torch.equal(last[k][0], v[lo:]), (mode, k)
+            assert not torch.equal(out['obs'], snap['obs']), 'produce() ran a new launch'
+            snap = {k: v.clone() for k, v in out.items()}
+    finally:
+        dist.destroy_process_group()
+
+
 def test_cfr_batched_past_refills(oracle):
     """Batched chance-sampling CFR for 1 000 iterations (each deals once per player, ~14.6 draws): every env's
     stream passes its staggered first refill ((e % 15) x 624 draws, cs_ring.h seed_blocks) by >= 300 draws. Tables
