@@ -165,7 +165,9 @@ int cs_action_features(cs_handle* h, const int32_t* ids, int64_t count, void* fe
  * double [2700][4] (policy initialised to 0.25 = the reference's row for an unseen key), flags uint32 [2700] (bit 0:
  * key in policy, bit 1: key in regrets and average_policy), zero-initialised. iteration0 = the agent's iteration
  * count before this call. A 1-env handle is the reference agent, bit-exact (same fp64 operation order); with more
- * envs, each deals its own game per player per iteration and the tables accumulate in fp64 atomics. Leduc only. */
+ * envs, each deals its own game per player per iteration and the tables add the deals' terms in one fixed order
+ * (records sorted by infoset, then a sequential sum per segment: bit-exact with the oracle and run to run,
+ * cs_cfr.hip). Leduc only. */
 int cs_cfr_train(cs_handle* h, int32_t iterations, int64_t iteration0, double* policy, double* average_policy,
                  double* regrets, uint32_t* flags, void* stream);
 

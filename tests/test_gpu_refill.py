@@ -63,9 +63,10 @@ def test_leduc_bench_shape_past_refills(oracle, flags):
 
 @pytest.mark.parametrize('game,T,launches', [('limit-holdem', 128, 10), ('no-limit-holdem', 128, 10),
                                              ('blackjack', 64, 9)])
-def test_lane_games_bench_shape_past_refills(oracle, game, T, launches):
-    """The other lane-per-env games at their bench T: each env draws ~25-57 words per step, so a few launches
-    cross several refills (every slot of the ring is rewritten at least twice)."""
+def test_lane_games_past_refills(oracle, game, T, launches):
+    """The other lane-per-env games over many chained launches (T below their bench T of 512 / 512 / 128, so that
+    the oracle stays fast; the bench T itself is test_full_size_after_precondition's): each env draws ~25-57 words
+    per step, so a few launches cross several refills (every slot of the ring is rewritten at least twice)."""
     _roll_past_refills(oracle, game, 2048 + 19, T, launches, 0, 42, past_refills(2))
 
 
@@ -79,7 +80,7 @@ def test_doudizhu_past_mt_twists(oracle):
                                       ('blackjack', 256), ('doudizhu', 48)])
 def test_full_size_after_precondition(oracle, game, win):
     """Every bench.py shape exactly as bench.py runs it: the BASELINE env count and fused steps per launch
-    (bench.GAMES: Leduc 2^20 x 256, Limit / No-limit 262 144 x 256, Blackjack 2^20 x 64, DouDizhu 65 536 x 64), the
+    (bench.GAMES: Leduc 2^20 x 256, Limit / No-limit 262 144 x 512, Blackjack 2^20 x 128, DouDizhu 65 536 x 64), the
     same seeds and policy, bench.precondition_launches untimed launches, then one timed-shape launch compared with the
     oracle on three windows (start, middle, end) replayed from seeding with the same global env ids. Every env of a
     window has passed its first refill (hold'em deal queues, Blackjack's shoe draws and DouDizhu's word window
