@@ -97,6 +97,13 @@ for step in "$@"; do
       g=${a[1]}; n=${a[2]}; t=${a[3]}; d=$O/pmc_${g}_$(echo "${a[@]:4}" | tr ' ' '_' | cut -c1-60); mkdir -p "$d"
       run 120 "$d/run.log" rocprofv3 --pmc ${a[@]:4} --output-format csv -d "$d/p" -o p -- python3 tools/ab_rollout.py "$g" "$n" "$t" 0
       python3 tools/pmc_summary.py "$d" > "$d/summary.txt" 2>&1; grep -A 12 k_rollout "$d/summary.txt" | head -30 ;;
+    tlb)        # tlb:GAME:INST:CTR1[:CTR2..]  per-allocation k_rollout time vs counters (tools/tlb_probe.py, one PMC pass)
+      g=${a[1]}; ni=${a[2]}; d=$O/tlb_${g}_$(echo "${a[@]:3}" | tr ' ' '_' | cut -c1-60); mkdir -p "$d"
+      run 300 "$d/run.log" rocprofv3 --pmc ${a[@]:3} --output-format csv -d "$d/p" -o p -- python3 tools/tlb_probe.py "$g" "$ni" 6
+      python3 tools/tlb_summary.py "$d" 6 > "$d/summary.txt" 2>&1; cat "$d/summary.txt"; grep instance "$d/run.log" ;;
+    tlbt)       # tlbt:GAME:INST  the same probe without a profiler (event times per allocation)
+      run 300 "$O/tlbt_${a[1]}.log" python3 tools/tlb_probe.py "${a[1]}" "${a[2]}" 6
+      cat "$O/tlbt_${a[1]}.log" ;;
     ceiling)
       run 300 "$O/ceiling.json" python3 tools/calib.py --ceiling
       cat "$O/ceiling.json" ;;
