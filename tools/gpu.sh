@@ -101,6 +101,15 @@ for step in "$@"; do
       g=${a[1]}; ni=${a[2]}; d=$O/tlb_${g}_$(echo "${a[@]:3}" | tr ' ' '_' | cut -c1-60); mkdir -p "$d"
       run 300 "$d/run.log" rocprofv3 --pmc ${a[@]:3} --output-format csv -d "$d/p" -o p -- python3 tools/tlb_probe.py "$g" "$ni" 6
       python3 tools/tlb_summary.py "$d" 6 > "$d/summary.txt" 2>&1; cat "$d/summary.txt"; grep instance "$d/run.log" ;;
+    place)      # place:GAME:MODE:K  which allocation's placement sets the time (tools/place_probe.py)
+      run 300 "$O/place_${a[1]}_${a[2]}.log" python3 tools/place_probe.py "${a[1]}" "${a[2]}" "${a[3]}"
+      grep -v amdgpu.ids "$O/place_${a[1]}_${a[2]}.log" ;;
+    place2)     # place2:GAME:WHAT:K  which trajectory tensor's placement matters (tools/place_probe2.py)
+      run 300 "$O/place2_${a[1]}_${a[2]}.log" python3 tools/place_probe2.py "${a[1]}" "${a[2]}" "${a[3]}"
+      grep -v amdgpu.ids "$O/place2_${a[1]}_${a[2]}.log" ;;
+    fill)       # fill:GIB:K  plain write / read rates of K allocations (tools/fill_probe.py)
+      run 300 "$O/fill_${a[1]}_${a[2]}.log" python3 tools/fill_probe.py "${a[1]}" "${a[2]}"
+      grep -v amdgpu.ids "$O/fill_${a[1]}_${a[2]}.log" ;;
     tlbt)       # tlbt:GAME:INST  the same probe without a profiler (event times per allocation)
       run 300 "$O/tlbt_${a[1]}.log" python3 tools/tlb_probe.py "${a[1]}" "${a[2]}" 6
       cat "$O/tlbt_${a[1]}.log" ;;
