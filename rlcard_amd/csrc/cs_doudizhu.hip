@@ -1236,13 +1236,39 @@ __device__ __forceinline__ void deal_half(int j, Env& e, uint32_t& dlo, uint32_t
     }
 }
 
+// k_rollout2's arguments, one struct: the kernel reads them from the kernarg segment through a pointer that every step
+// makes opaque again (PairArgsK), so a field is a scalar load where the step uses it. Taken as separate arguments
+// (the table alone 24 SGPRs, the outputs 14) they stayed live in SGPRs for the whole kernel, were spilled to VGPR
+// lanes and restored with v_readlane -- a VALU instruction -- at every use (153 spilled SGPRs, 417 restores in the
+// step loop).
+struct PairArgs {
+    uint32_t* mt;
+    uint32_t* ctl;
+    uint32_t* st;
+    int64_t n;
+    uint64_t seed, t0, env_base;
+    cs_traj_out out;
+    Tab tb;
+    int32_t T, kfl;
+};
+typedef const __attribute__((address_space(4))) PairArgs* PairArgsK;
+
 template <bool PHX>
-__global__ __launch_bounds__(PBLOCK, CS_DDZ_PAIR_MINW) void k_rollout2(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n, int T,
-                                                     uint64_t seed, uint64_t t0, uint64_t env_base, cs_traj_out out,
-                                                     Tab tb, int kfl)
+__global__ __launch_bounds__(PBLOCK, CS_DDZ_PAIR_MINW) void k_rollout2(PairArgs args)
 {
+    PairArgsK ak = (PairArgsK)__builtin_amdgcn_kernarg_segment_ptr();
+    auto arg = [&]() -> const PairArgs& {
+        asm volatile("" : "+s"(ak));
+        return *(const PairArgs*)ak;
+    };
+    uint32_t* const mt = args.mt;
+    uint32_t* const ctl = args.ctl;
+    uint32_t* const st = args.st;
+    const int64_t n = args.n;
+    const int T = args.T, kfl = args.kfl;
     __shared__ PairLds lds[PWPB][2];
     __shared__ TabLds tl;
+    const Tab& tb = arg().tb;
     load_tab(tl, tb);                 // every thread of the block, before any wave leaves
     const int lane = (int)(threadIdx.x & (WAVE - 1)), hl = lane & (HW - 1), hf = lane >> 5;
     const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
@@ -1304,10 +1330,14 @@ __global__ __launch_bounds__(PBLOCK, CS_DDZ_PAIR_MINW) void k_rollout2(uint32_t*
         for (int j = 0; j < 2; j++)
             if ((need >> (HW * j)) & 1u) deal_half<PHX>(j, e, dlo, dhi, pm, mt, env, lane);
     }
-    const uint64_t genv = env_base + (uint64_t)env;
+    const uint64_t genv = args.env_base + (uint64_t)env;
     uint32_t rr_lane = 0;
     bool dirty = true;   // CS_DDZ_CLEAN: the half's image holds bits the previous step did not clean
     for (int t = 0; t < T; t++) {
+        const PairArgs& A = arg();
+        const Tab& tb = A.tb;
+        const cs_traj_out& out = A.out;
+        const uint64_t seed = A.seed, t0 = A.t0;
         const int64_t row = (int64_t)t * n + env;
         if (CS_DDZ_CLEAN == 0 || __ballot(dirty)) {   // zero the mask image of both envs: 224 uint4 each, 32 lanes per env
             uint4* z = (uint4*)L.mask;
@@ -1486,12 +1516,9 @@ hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t
 {
     if constexpr (CS_DDZ_PAIR) {
         const dim3 g((unsigned)((b.n + 2 * PWPB - 1) / (2 * PWPB)));
-        if (b.rng_mode == CS_RNG_PHILOX)
-            hipLaunchKernelGGL(k_rollout2<true>, g, dim3(PBLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0, env_base, o,
-                               *(const Tab*)b.table, b.serial_refill);
-        else
-            hipLaunchKernelGGL(k_rollout2<false>, g, dim3(PBLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0, env_base, o,
-                               *(const Tab*)b.table, b.serial_refill);
+        const PairArgs a{b.mt, b.ctl, b.state, b.n, seed, t0, env_base, o, *(const Tab*)b.table, T, b.serial_refill};
+        if (b.rng_mode == CS_RNG_PHILOX) hipLaunchKernelGGL(k_rollout2<true>, g, dim3(PBLOCK), 0, s, a);
+        else hipLaunchKernelGGL(k_rollout2<false>, g, dim3(PBLOCK), 0, s, a);
         return hipGetLastError();
     }
     if (b.rng_mode == CS_RNG_PHILOX)

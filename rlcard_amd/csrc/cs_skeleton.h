@@ -529,11 +529,40 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n
     step_record<G>(rec, st, n, c);
 }
 
+// k_rollout's arguments as one struct, read from the kernarg segment through a pointer that every step makes opaque
+// again (RolloutArgsK): the loop's uses (outputs, policy key, flags) are scalar loads where the step needs them instead
+// of SGPRs live for the whole kernel, which the compiler spilled to VGPR lanes and restored with v_readlane (a VALU
+// instruction) at every use (ddz::PairArgs, the same for DouDizhu)
+struct RolloutArgs {
+    uint32_t* mt;
+    uint32_t* ctl;
+    uint32_t* st;
+    int64_t n;
+    uint64_t seed, t0, env_base;
+    cs_traj_out out;
+    GameParams prm;
+    uint32_t* sctl;
+    uint8_t* sbuf;
+    int32_t T, flags;
+};
+typedef const __attribute__((address_space(4))) RolloutArgs* RolloutArgsK;
+
 template <class G>
-__global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n, int T,
-                                                    uint64_t seed, uint64_t t0, uint64_t env_base, cs_traj_out out,
-                                                    int flags, GameParams prm, uint32_t* sctl, uint8_t* sbuf)
+__global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs args)
 {
+    RolloutArgsK ak = (RolloutArgsK)__builtin_amdgcn_kernarg_segment_ptr();
+    auto arg = [&]() -> const RolloutArgs& {
+        asm volatile("" : "+s"(ak));
+        return *(const RolloutArgs*)ak;
+    };
+    uint32_t* const mt = args.mt;
+    uint32_t* const ctl = args.ctl;
+    uint32_t* const st = args.st;
+    const int64_t n = args.n;
+    const int T = args.T, flags = args.flags;
+    const GameParams prm = args.prm;
+    uint32_t* const sctl = args.sctl;
+    uint8_t* const sbuf = args.sbuf;
     CS_SMEM_ROWS(G, G::EPW);
     __shared__ __attribute__((aligned(16))) uint8_t stage[WAVES_PER_BLOCK][StageBytes<G>::value];
     const LaneCtx c = lane_ctx<G::EPW>(n);
@@ -582,16 +611,22 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(uint32_t* mt, u
     }
     refill<G>(m, c.lane, flags & 1);
     if (staged) restage<G>(m, stage[c.wid], c.lane, c.valid);
-    uint8_t* obs = (uint8_t*)out.obs;
-    uint8_t* legal = (uint8_t*)out.legal;
-    uint8_t* player = (uint8_t*)out.player;
-    float* reward = (float*)out.reward;
-    uint8_t* done_o = (uint8_t*)out.done;
-    const uint64_t genv = env_base + (uint64_t)c.env;
+    const uint64_t genv = args.env_base + (uint64_t)c.env;
     PolicyRng pol;
     for (int t = 0; t < T; t++) {
+        const RolloutArgs& A = arg();
+        const cs_traj_out& out = A.out;
+        uint8_t* obs = (uint8_t*)out.obs;
+        uint8_t* legal = (uint8_t*)out.legal;
+        uint8_t* player = (uint8_t*)out.player;
+        float* reward = (float*)out.reward;
+        uint8_t* done_o = (uint8_t*)out.done;
+        const uint64_t seed = A.seed, t0 = A.t0;
 
-        const int64_t rowbase = (int64_t)t * n;
+#ifndef CS_TPAD
+#define CS_TPAD 0   // profiling builds only: trajectory rows of step t start at t * (n + CS_TPAD) (tools/place_probe.py)
+#endif
+        const int64_t rowbase = (int64_t)t * (n + CS_TPAD);
         const int p = g.current();
         const uint64_t lg = g.legal();
         uint32_t bits[G::NB];
@@ -729,8 +764,8 @@ template <class G>
 static hipError_t rollout_g(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
                             const cs_traj_out& o, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_rollout<G>, grid_for(b.n, G::EPW), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0,
-                       env_base, o, b.serial_refill, params_of(b), b.sctl, b.sbuf);
+    const RolloutArgs a{b.mt, b.ctl, b.state, b.n, seed, t0, env_base, o, params_of(b), b.sctl, b.sbuf, T, b.serial_refill};
+    hipLaunchKernelGGL(k_rollout<G>, grid_for(b.n, G::EPW), dim3(BLOCK), 0, s, a);
     return hipGetLastError();
 }
 
