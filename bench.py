@@ -185,6 +185,9 @@ def main():
                     help='skip the CS_RNG_PHILOX phase (reported under "rng_philox")')
     ap.add_argument('--no-precondition', dest='precondition', action='store_false',
                     help='time from freshly seeded streams (optimistic: no MT block refills yet)')
+    ap.add_argument('--placement', type=int, default=3,
+                    help='N=1: time a few launches into this many fresh trajectory allocations after the timed region '
+                         '(untimed context under "placement"; 0: off)')
     ap.add_argument('--no-device-state', dest='device_state', action='store_false',
                     help='skip the amd-smi / HIP attribute sample of the box (reported under "device")')
     args = ap.parse_args()
@@ -273,6 +276,31 @@ def main():
     if rank == 0 and args.device_state:
         sampler.join(timeout=60)   # the amd-smi query may outlast a short timed region
 
+    placement = None
+    if world == 1 and args.placement > 0:
+        # untimed context for `value` ("the 3.5 / 4.3 ms split"): the same launches into fresh trajectory
+        # allocations -- the kernel time follows where the output buffers land in HBM, so a single allocation's
+        # time is one draw from this spread
+        per = [kernel_ms]
+        for _ in range(args.placement):
+            other = env.new_traj_out(T)
+            ms = []
+            for k in range(4):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                env.rollout(T, policy_seed=5, t0=t_launch * T, out=other)
+                e1.record(stream)
+                t_launch += 1
+                torch.cuda.synchronize()
+                ms.append(e0.elapsed_time(e1))
+            per.append(sorted(ms)[len(ms) // 2] if len(ms) % 2 else sum(sorted(ms)[1:3]) / 2)
+            del other
+        placement = dict(kernel_ms_per_allocation=per,
+                         note='untimed: kernel ms per launch of the timed allocation (first) and of %d fresh '
+                              'trajectory allocations (median of 4 launches each); not part of value'
+                              % args.placement)
+        torch.cuda.empty_cache()
+
     gather_info = {}
     if world > 1 and args.gather != 'none':
         # the trajectory exchange: rollout + exchange per step, timed like the main loop
@@ -360,6 +388,8 @@ def main():
                                   smi={k: smi.get(k) for k in keep},
                                   partition=(smi.get('partition') or {}).get('current_partition'),
                                   timed_window=power)
+        if placement is not None:
+            line['placement'] = placement
         line.update(gather_info)
         if philox_info is not None:
             line['rng_philox'] = philox_info

@@ -40,7 +40,8 @@ constexpr int MASK_WORDS = MASK_PAD + KTH_LANES * KTH_WORDS + MASK_PAD;
 constexpr int NSEG = 20;                          // 54-bit obs blocks (16 used) + zero tail
 constexpr int BV_WORDS = 32;                      // obs bits (912 + 16 front pad) as dwords
 #ifndef CS_PROF_DDZ
-#define CS_PROF_DDZ 0   // profiling only (wrong outputs): 1 skip legal rows, 2 skip obs rows, 4 skip build_obs
+#define CS_PROF_DDZ 0   // profiling only (wrong outputs): 1 skip legal rows, 2 skip obs rows, 4 skip build_obs (one-env
+                        // kernels), 16 skip build_obs2 (pair kernel)
 #endif
 
 constexpr int LIST_RING = 128;                    // the step's tested mask dwords (a ring: see build_legal)
@@ -1352,7 +1353,7 @@ __global__ __launch_bounds__(PBLOCK, CS_DDZ_PAIR_MINW) void k_rollout2(PairArgs 
         const Cand cd = cand_of(e, tb, tl);
         const Fast fst = fast_issue(e, cd, tb, L, lane, valid && (kfl & 1) == 0);   // kernel flag bit 0: A/B only
         Legal lg = build_legal2(e, cd, tb, tl, L, lmis, lane, valid && !fst.fast);
-        build_obs2(e, e.cur, L, lane);
+        if (!(CS_PROF_DDZ & 16)) build_obs2(e, e.cur, L, lane);   // profiling builds only: bit 4 skips the obs image
         if (__ballot(fst.fast)) fast_finish(fst, e.hand(e.cur), tb, L, lmis, lane, lg);
         wave_sync_lds();
         const uint32_t count = lg.total + (cd.leading ? 0u : 1u);

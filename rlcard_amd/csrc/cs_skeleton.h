@@ -623,10 +623,7 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
         uint8_t* done_o = (uint8_t*)out.done;
         const uint64_t seed = A.seed, t0 = A.t0;
 
-#ifndef CS_TPAD
-#define CS_TPAD 0   // profiling builds only: trajectory rows of step t start at t * (n + CS_TPAD) (tools/place_probe.py)
-#endif
-        const int64_t rowbase = (int64_t)t * (n + CS_TPAD);
+        const int64_t rowbase = (int64_t)t * n;
         const int p = g.current();
         const uint64_t lg = g.legal();
         uint32_t bits[G::NB];

@@ -7,7 +7,6 @@ alive (so each is its own physical memory), timed in interleaved rounds in one p
 
 Each line: the allocation, its median launch time per round (HIP events), and the buffers' device addresses.
 """
-import os
 import statistics
 import sys
 
@@ -28,23 +27,8 @@ def make_env():
     return v
 
 
-TPAD = int(os.environ.get('AP_TPAD', '0'))   # a CS_TPAD=... library: step t's rows start at t * (n + TPAD)
-
-
-def new_traj():
-    if not TPAD:
-        return envs[0].new_traj_out(T)
-    v, m, d = envs[0], n + TPAD, envs[0].device   # [T, n + TPAD, ...] storage; the kernel's rows are n long
-    return dict(obs=torch.empty((T, m, v.obs_dim), dtype=torch.uint8, device=d),
-                legal=torch.empty((T, m, v.legal_bytes), dtype=torch.uint8, device=d),
-                player=torch.empty((T, m), dtype=torch.uint8, device=d),
-                reward=torch.empty((T, m, v.num_players), dtype=torch.float32, device=d),
-                done=torch.empty((T, m), dtype=torch.uint8, device=d),
-                action=torch.empty((T, m), dtype=v.action_dtype, device=d))
-
-
 envs = [make_env() for _ in range(K if mode in ('env', 'both') else 1)]
-trajs = [new_traj() for _ in range(K if mode in ('traj', 'both') else 1)]
+trajs = [envs[0].new_traj_out(T) for _ in range(K if mode in ('traj', 'both') else 1)]
 pairs = [(envs[i if len(envs) > 1 else 0], trajs[i if len(trajs) > 1 else 0]) for i in range(K)]
 pre = bench.precondition_launches(game, T, envs[0])
 t = {id(v): 0 for v in envs}
