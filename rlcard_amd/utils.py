@@ -1,5 +1,6 @@
 """Host utilities with the behaviour of rlcard/utils/utils.py that examples call around the env path (run_random.py,
-run_cfr.py, run_rl.py): set_seed, reorganize, remove_illegal, tournament. The batched, on-device forms of reorganize
+run_cfr.py, run_rl.py): set_seed, reorganize, remove_illegal, tournament; and of rlcard/utils/pettingzoo_utils.py
+(wrap_state, run_game_pettingzoo, reorganize_pettingzoo, tournament_pettingzoo). The batched, on-device forms of reorganize
 and of the legal-id lists are VecEnv.transitions / VecEnv.legal_lists (include/cardsim.h)."""
 import random
 
@@ -57,3 +58,60 @@ def tournament(env, num):
             total += np.asarray(pay, dtype=np.float64)[:env.num_players]
             games += 1
     return list(total / games)
+
+
+# ---- PettingZoo-side helpers (rlcard/utils/pettingzoo_utils.py:5-72) --------------------------------------------------
+# They drive any env with PettingZoo's AEC protocol: reset(), agent_iter(), last() -> (observation, reward, termination,
+# truncation, info), step(action); observations are {'observation': ..., 'action_mask': ...}. pettingzoo itself is not
+# installed here: rlcard_amd.envs.pettingzoo.AECEnv gives the engine's envs that protocol.
+
+def wrap_state(state):
+    """Behaviour of pettingzoo_utils.py:5-17: an AEC observation dict as an rlcard state (obs, legal_actions with None
+    values in ascending id order, raw_legal_actions = the same ids); an rlcard state passes through unchanged."""
+    if 'obs' in state and 'legal_actions' in state and 'raw_legal_actions' in state:
+        return state
+    ids = np.flatnonzero(state['action_mask'])
+    legal = dict.fromkeys(ids)
+    return {'obs': state['observation'], 'legal_actions': legal, 'raw_legal_actions': list(legal)}
+
+
+def run_game_pettingzoo(env, agents, is_training=False):
+    """Behaviour of pettingzoo_utils.py:20-37: one episode; per agent name the list alternates (observation, reward,
+    done) records and the action taken after each (None once the agent is done)."""
+    from collections import defaultdict
+    env.reset()
+    traj = defaultdict(list)
+    for name in env.agent_iter():
+        obs, reward, done, _, _ = env.last()   # termination only, as the reference reads it
+        traj[name].append((obs, reward, done))
+        if done:
+            act = None
+        elif is_training:
+            act = agents[name].step(obs)
+        else:
+            act = agents[name].eval_step(obs)[0]
+        traj[name].append(act)
+        env.step(act)
+    return traj
+
+
+def reorganize_pettingzoo(trajectories):
+    """Behaviour of pettingzoo_utils.py:40-61: [obs, action, reward, next_obs, done] per consecutive record pair, the
+    reward and done taken from the later record."""
+    from collections import defaultdict
+    out = defaultdict(list)
+    for name, seq in trajectories.items():
+        for k in range(0, len(seq) - 2, 2):
+            nxt = seq[k + 2]
+            out[name].append([seq[k][0], seq[k + 1], nxt[1], nxt[0], nxt[2]])
+    return out
+
+
+def tournament_pettingzoo(env, agents, num_episodes):
+    """Behaviour of pettingzoo_utils.py:64-72: mean over episodes of each agent's summed transition rewards."""
+    from collections import defaultdict
+    total = defaultdict(float)
+    for _ in range(num_episodes):
+        for name, trans in reorganize_pettingzoo(run_game_pettingzoo(env, agents)).items():
+            total[name] += sum(t[2] for t in trans)
+    return {name: r / num_episodes for name, r in total.items()}

@@ -28,6 +28,8 @@ Fixtures written:
   holdem_ref_kats.npz  the reference's own compare_hands known answers (tests/utils/test_holdem_utils.py), recorded.
   ddz_judger.npz   (hand, previous play) -> legal id sets from Judger / get_gt_cards (doudizhu/judger.py, utils.py),
                    plus the reference test's full-deck case (tests/games/test_doudizhu_judger.py:146-156).
+  pettingzoo.json  rlcard/utils/pettingzoo_utils.py and RandomAgentPettingZoo over tests/fake_aec.py (episodes,
+                   reorganized transitions, tournament means, wrap_state); JSON because the records are ragged.
 
 Usage:  python tests/golden/gen_golden.py [--only NAME ...]
 """
@@ -748,6 +750,61 @@ def gen_ddz_judger():
     print('ddz_judger.npz: %d cases, %d legal ids' % (len(hands), len(ids)))
 
 
+def pz_record(traj):
+    # per agent: [[observation, action_mask, reward, done], action (-1 = None), ...] as JSON lists
+    out = {}
+    for name, seq in traj.items():
+        rec = []
+        for k, item in enumerate(seq):
+            if k % 2 == 0:
+                obs, reward, done = item
+                rec.append([np.asarray(obs['observation']).tolist(), np.asarray(obs['action_mask']).tolist(),
+                            float(reward), bool(done)])
+            else:
+                rec.append(-1 if item is None else int(item))
+        out[name] = rec
+    return out
+
+
+def gen_pettingzoo():
+    # rlcard/utils/pettingzoo_utils.py + agents/pettingzoo_agents.py driven over tests/fake_aec.py (an AEC env of our
+    # own; pettingzoo is not installed): episodes (train and eval picks), reorganized transitions, tournament means,
+    # wrap_state of AEC observations
+    sys.path.insert(0, os.path.dirname(OUT))
+    from fake_aec import FakeAEC
+    from rlcard.utils.pettingzoo_utils import (wrap_state, run_game_pettingzoo, reorganize_pettingzoo,
+                                               tournament_pettingzoo)
+    from rlcard.agents.pettingzoo_agents import RandomAgentPettingZoo
+    cases = []
+    for players, actions, seed in [(2, 4, 1), (3, 5, 2), (4, 3, 7)]:
+        env = FakeAEC(players, actions, 4, seed)
+        agents = {a: RandomAgentPettingZoo(num_actions=actions) for a in env.possible_agents}
+        np.random.seed(seed)
+        eps = []
+        for e in range(6):
+            traj = run_game_pettingzoo(env, agents, is_training=(e % 2 == 0))
+            re = reorganize_pettingzoo(traj)
+            eps.append({'traj': pz_record(traj),
+                        'reorg': {n: [[int(t[1]) if t[1] is not None else -1, float(t[2]), bool(t[4]),
+                                       np.asarray(t[0]['observation']).tolist(),
+                                       np.asarray(t[3]['observation']).tolist()] for t in ts]
+                                  for n, ts in re.items()}})
+        tour = tournament_pettingzoo(env, agents, 5)
+        cases.append({'players': players, 'actions': actions, 'seed': seed, 'episodes': eps,
+                      'tournament': {k: float(v) for k, v in tour.items()}})
+    wraps = []
+    rng = np.random.RandomState(5)
+    for _ in range(8):
+        mask = (rng.rand(7) < 0.5).astype(np.int8)
+        obs = rng.randint(0, 4, size=3).astype(np.float32)
+        w = wrap_state({'observation': obs, 'action_mask': mask})
+        wraps.append({'mask': mask.tolist(), 'obs': obs.tolist(), 'legal': [int(x) for x in w['legal_actions']],
+                      'raw_legal': [int(x) for x in w['raw_legal_actions']]})
+    with open(os.path.join(OUT, 'pettingzoo.json'), 'w') as f:
+        json.dump({'cases': cases, 'wrap_state': wraps}, f)
+    print('pettingzoo.json', len(cases), 'cases')
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--only', nargs='*', default=None)
@@ -756,7 +813,8 @@ def main():
     gens = {'mt19937': gen_mt, 'leduc': gen_leduc, 'limit': gen_limit, 'blackjack': gen_blackjack,
             'doudizhu': gen_doudizhu, 'nolimit': gen_nolimit, 'cfr': gen_cfr, 'holdem_eval': gen_holdem_eval,
             'holdem_ref_kats': gen_holdem_ref_kats, 'ddz_table': gen_ddz_table,
-            'ddz_judger': gen_ddz_judger, 'nplayer': gen_nplayer, 'raw': gen_raw, 'blackjack_shoe': gen_blackjack_shoe}
+            'ddz_judger': gen_ddz_judger, 'nplayer': gen_nplayer, 'raw': gen_raw, 'blackjack_shoe': gen_blackjack_shoe,
+            'pettingzoo': gen_pettingzoo}
     for name, fn in gens.items():
         if args.only is None or name in args.only:
             fn()
