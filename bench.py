@@ -30,7 +30,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH
 MT_N = 624              # words per MT19937 block
 
 # per game: default envs per GPU (BASELINE.json configs), default fused steps per launch, packed state bytes per env
-# read + written once per launch (state words + the RNG control word), the expected tempered-u32 MT19937 draws per
+# read + written once per launch (state words + the RNG control word; hold'em: 4 game words + the 8-deal queue), the expected tempered-u32 MT19937 draws per
 # env-step under random play (exact acceptance rates of random_interval x random-play game lengths). The
 # stream geometry (draws before the first refill, draws per refill) comes from the built library (VecEnv.rng_period:
 # the byte ring's CS_RING_SLOTS, or DouDizhu's two-block word window), see precondition_launches.
@@ -39,11 +39,11 @@ MT_N = 624              # words per MT19937 block
 # kernel), Blackjack 128 vs 64 +2 %.
 GAMES = {
     'leduc-holdem': dict(envs=1 << 20, T=256, state_bytes=2 * 4 + 4, draws_per_step=2.83),
-    'limit-holdem': dict(envs=262144, T=512, state_bytes=12 * 4 + 4, draws_per_step=24.5),
+    'limit-holdem': dict(envs=262144, T=512, state_bytes=21 * 4 + 4, draws_per_step=24.5),
     'blackjack': dict(envs=1 << 20, T=128, state_bytes=20 * 4 + 4, draws_per_step=57.0),
     'doudizhu': dict(envs=65536, T=64, state_bytes=36 * 4 + 4, draws_per_step=1.21),
     # not a BASELINE config; draws/step counted on the oracle (4096 envs x 256 random steps)
-    'no-limit-holdem': dict(envs=262144, T=512, state_bytes=4 * 4 + 4, draws_per_step=26.3),
+    'no-limit-holdem': dict(envs=262144, T=512, state_bytes=21 * 4 + 4, draws_per_step=26.3),
 }
 TIMED_TARGET_S = 2.0     # default --steps: enough launches for >= ~2 s of timed region (box variance, SMI sampler)
 

@@ -35,13 +35,16 @@
 #define CS_LIMIT_RESTAGE_B 8
 #endif
 #ifndef CS_LIMIT_MIN_WAVES
-#define CS_LIMIT_MIN_WAVES 5
+#define CS_LIMIT_MIN_WAVES 4   // the LDS of a deal queue of 8 allows 4 blocks of 4 waves per CU
 #endif
 #ifndef CS_LIMIT_STAGE_RF
 #define CS_LIMIT_STAGE_RF 120   // batched restage: 2.70 -> 2.65 ms per 128-step launch (R 80 / RF 100 or 124 the same)
 #endif
 #ifndef CS_LIMIT_DQ_REGS
 #define CS_LIMIT_DQ_REGS 0
+#endif
+#ifndef CS_LIMIT_DQ_HBM
+#define CS_LIMIT_DQ_HBM 0   // rollout: the deal queue read and written in place in the env state (HBM), no LDS copy
 #endif
 #ifndef CS_LIMIT_SPARSE_OBS
 #define CS_LIMIT_SPARSE_OBS 1   // rollout obs rows through row_write_sparse (0: the expanded bitmap, RowWriter)
@@ -392,21 +395,26 @@ __device__ __forceinline__ uint32_t holdem_showdown(uint32_t holes, uint32_t boa
 // rollout draws deals ahead -- one pass of all lanes with room in their queue, in lockstep, whenever a lane ends a
 // game with its queue empty -- instead of a pass at every step in which any lane of the wave resets (a 32-env wave
 // has a reset almost every step, with ~2/5 of its lanes active). Same deals in the same stream order, so outputs are
-// unchanged. The queue lives after the game's words in the env state: a header (count:3, head:2, no-limit dealer
-// drawn << 5, dealer << 6, draws[8:7] of slot k << 7 + 2 k) and DQ entries of two words (e0 = holes | seat bit << 24 |
-// draws[6:0] << 25, e1 = board | showdown << 30; draws = MT words the deal consumed, for the host's stream position,
-// saturating at 511).
+// unchanged. The queue lives after the game's words in the env state: a header (count:CB, head:CB-1, no-limit dealer
+// drawn << XB, dealer << XB + 1, draws[8:7] of slot k << XB + 2 + 2 k; CB = log2(DQ) + 1, XB = 2 CB - 1: DQ 4 -> 3, 5;
+// DQ 8 -> 4, 7) and DQ entries of two words (e0 = holes | seat bit << 24 | draws[6:0] << 25, e1 = board | showdown
+// << 30; draws = MT words the deal consumed, for the host's stream position, saturating at 511).
 #ifndef CS_DEAL_QUEUE
-#define CS_DEAL_QUEUE 4
+#define CS_DEAL_QUEUE 8   // 8 vs 4 (LDS queue): 0.39 vs 0.46 deal passes per wave-step (simulated), the pass costs ~1 200
+                          // wave-instructions; with 4 waves per SIMD instead of 5: Limit -2.5 %, No-limit -0.7 %
 #endif
 constexpr int HOLDEM_DQ = CS_DEAL_QUEUE;
-static_assert(HOLDEM_DQ == 0 || HOLDEM_DQ == 2 || HOLDEM_DQ == 4, "deal queue: 2-bit head, power-of-two ring");
+static_assert(HOLDEM_DQ == 0 || HOLDEM_DQ == 2 || HOLDEM_DQ == 4 || HOLDEM_DQ == 8, "deal queue: power-of-two ring");
 constexpr int HOLDEM_DQ_WORDS = HOLDEM_DQ > 0 ? 1 + 2 * HOLDEM_DQ : 0;
+constexpr int DQ_CB = HOLDEM_DQ == 8 ? 4 : HOLDEM_DQ == 4 ? 3 : 2;   // count bits (0..DQ)
+constexpr int DQ_XB = 2 * DQ_CB - 1;                                // first bit after count and head
+static_assert(DQ_XB + 2 + 2 * HOLDEM_DQ <= 32, "deal queue header fits a word");
 
 struct Limit {
     static constexpr int GW = 4;                        // game words; the deal queue follows
     static constexpr int DQ = HOLDEM_DQ;
     static constexpr bool DQ_REGS = CS_LIMIT_DQ_REGS;          // rollout: queue in registers, else LDS
+    static constexpr bool DQ_HBM = CS_LIMIT_DQ_HBM;            // rollout: queue in place in the state (HBM)
     static constexpr int OBS = 72, A = 4, P = 2, LB = 1, WORDS = GW + HOLDEM_DQ_WORDS, ACTION_BYTES = 1;
     static constexpr int NB = 3;
     static constexpr bool RING = true;          // MT stream as the byte ring (cs_ring.h)
@@ -416,7 +424,8 @@ struct Limit {
     static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = CS_LIMIT_STAGE_W, STAGE_PAD = 8, STAGE_R = CS_LIMIT_STAGE_R;
     static constexpr int STAGE_RF = CS_LIMIT_STAGE_RF;    // batch restage threshold (ring_restage_wave)
     static constexpr int RESTAGE_B = CS_LIMIT_RESTAGE_B;  // lanes restaged per pass (loads in flight)
-    static constexpr int MIN_WAVES = CS_LIMIT_MIN_WAVES;  // 5 waves/SIMD: beats 4 (no spills) and 6 (40 spilled VGPRs)
+    static constexpr int MIN_WAVES = CS_LIMIT_MIN_WAVES;  // 4 waves/SIMD (LDS-bound with the 8-deal queue; at a 4-deal
+                                                          // queue 5 beat 4 and 6, which spilled 40 VGPRs)
     static constexpr int EPW = CS_LIMIT_EPW;   // rollout envs per wave: 262 144 envs need half-full waves (lane_ctx)
     static constexpr int REFILL_K = 2;   // stale blocks twisted per pass (see mt_refill_wave)
     __device__ __forceinline__ void bind(uint32_t*, const GameParams&) {}

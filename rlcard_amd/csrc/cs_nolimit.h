@@ -40,6 +40,9 @@
 #ifndef CS_NOLIMIT_DQ_REGS
 #define CS_NOLIMIT_DQ_REGS 0
 #endif
+#ifndef CS_NOLIMIT_DQ_HBM
+#define CS_NOLIMIT_DQ_HBM 0
+#endif
 #ifndef CS_NOLIMIT_SPARSE_OBS
 #define CS_NOLIMIT_SPARSE_OBS 1   // rollout obs rows through row_write_sparse (0: RowWriterRaw of the expanded row)
 #endif
@@ -47,7 +50,7 @@
 #define CS_NOLIMIT_EPW 32
 #endif
 #ifndef CS_NOLIMIT_MIN_WAVES
-#define CS_NOLIMIT_MIN_WAVES 5
+#define CS_NOLIMIT_MIN_WAVES 4   // LDS-bound at 4 blocks per CU with the 8-deal queue
 #endif
 
 namespace cs {
@@ -56,6 +59,7 @@ struct Nolimit {
     static constexpr int GW = 4;                        // game words; the deal queue follows (cs_limit.h)
     static constexpr int DQ = HOLDEM_DQ;
     static constexpr bool DQ_REGS = CS_NOLIMIT_DQ_REGS;          // rollout: queue in registers, else LDS
+    static constexpr bool DQ_HBM = CS_NOLIMIT_DQ_HBM;            // rollout: queue in place in the state (HBM)
     static constexpr int OBS = 54, A = 5, P = 2, LB = 1, WORDS = GW + HOLDEM_DQ_WORDS, ACTION_BYTES = 1;
     static constexpr int NB = 14;               // raw obs bytes, four per word (RowWriterRaw)
     static constexpr bool RING = true;          // MT stream as the byte ring (cs_ring.h)
@@ -152,15 +156,15 @@ struct Nolimit {
     }
 
     // the dealer seat randint(0, 2) before the first game's shuffle (game.py:62-63; kept by later games of the env,
-    // hdr bits 5 / 6 of the deal queue header), then the hold'em deal
+    // hdr bits DQ_XB / DQ_XB + 1 of the deal queue header), then the hold'em deal
     template <class Rng>
     __device__ __forceinline__ void make_deal(Rng& rng, uint32_t& hdr, uint32_t& e0, uint32_t& e1) const
     {
         uint32_t dealer;
         if (dealer_cfg >= 0) dealer = (uint32_t)dealer_cfg;
-        else if ((hdr >> 5) & 1u) dealer = (hdr >> 6) & 1u;
+        else if ((hdr >> DQ_XB) & 1u) dealer = (hdr >> (DQ_XB + 1)) & 1u;
         else dealer = rng.interval(1u);
-        hdr = (hdr & ~0x60u) | 1u << 5 | dealer << 6;
+        hdr = (hdr & ~(3u << DQ_XB)) | 1u << DQ_XB | dealer << (DQ_XB + 1);
         holdem_deal2(rng, e0, e1);
         e1 |= holdem_showdown(e0, e1) << 30;
         e0 |= dealer << 24;
@@ -168,7 +172,7 @@ struct Nolimit {
     template <class Rng>
     __device__ __forceinline__ void reset(Rng& rng)
     {
-        uint32_t hdr = ((w0 >> 26) & 1u) << 5 | ((w0 >> 25) & 1u) << 6, e0, e1;   // drawn by an earlier game
+        uint32_t hdr = ((w0 >> 26) & 1u) << DQ_XB | ((w0 >> 25) & 1u) << (DQ_XB + 1), e0, e1;   // drawn earlier
         make_deal(rng, hdr, e0, e1);
         reset_from(e0, e1);
     }

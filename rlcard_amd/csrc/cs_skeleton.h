@@ -246,13 +246,15 @@ __device__ __forceinline__ uint32_t* scratch_of(uint32_t* wave_area, int lane)
 // ---- hold'em deal queue (cs_limit.h): q = the env's queue words, `stride` apart (state in HBM: n; LDS copy: 1) ------
 template <class G, class = void>
 struct DqOf {
-    static constexpr int value = 0, words = 0;
-    static constexpr bool regs = false;
+    static constexpr int value = 0, words = 0, cb = 0, xb = 0;
+    static constexpr bool regs = false, hbm = false;
 };
 template <class G>
 struct DqOf<G, std::void_t<decltype(G::DQ)>> {
     static constexpr int value = G::DQ, words = G::DQ > 0 ? 1 + 2 * G::DQ : 0;
-    static constexpr bool regs = G::DQ_REGS;
+    // header fields (cs_limit.h): count bits, then head bits (cb - 1), from bit xb the dealer bits and draws[8:7]
+    static constexpr int cb = G::DQ == 8 ? 4 : G::DQ == 4 ? 3 : 2, xb = 2 * cb - 1;
+    static constexpr bool regs = G::DQ_REGS, hbm = G::DQ_HBM;
 };
 
 // queue word views: DqMem = words `stride` apart (state in HBM: n; LDS copy: 1), DqRegs = the words in registers
@@ -284,28 +286,32 @@ struct DqRegs {
 template <class G, class Rng, class Q>
 __device__ __forceinline__ void dq_push(const G& g, Rng& rng, Q& q)
 {
+    constexpr int CB = DqOf<G>::cb, XB = DqOf<G>::xb;
+    constexpr uint32_t CM = (1u << CB) - 1u, HM = (uint32_t)G::DQ - 1u;
     uint32_t hdr = q.get(0);
-    const uint32_t cnt = hdr & 7u, head = (hdr >> 3) & 3u, p0 = rng.pos;
+    const uint32_t cnt = hdr & CM, head = (hdr >> CB) & HM, p0 = rng.pos;
     uint32_t e0, e1;
     g.make_deal(rng, hdr, e0, e1);
     uint32_t d = rng.pos >= p0 ? rng.pos - p0 : rng.pos + (uint32_t)RING - p0;
     d = d < 511u ? d : 511u;
-    const uint32_t slot = (head + cnt) & (uint32_t)(G::DQ - 1), hi = 7u + 2u * slot;
+    const uint32_t slot = (head + cnt) & HM, hi = (uint32_t)XB + 2u + 2u * slot;
     q.set(1 + 2 * slot, e0 | (d & 127u) << 25);
     q.set(2 + 2 * slot, e1);
-    q.set(0, (hdr & ~7u & ~(3u << hi)) | (d >> 7) << hi | (cnt + 1u));
+    q.set(0, (hdr & ~CM & ~(3u << hi)) | (d >> 7) << hi | (cnt + 1u));
 }
 
 // Game.init_game: the oldest queued deal, or a deal drawn now when the queue is empty
 template <class G, class Rng, class Q>
 __device__ __forceinline__ void dq_reset(G& g, Rng& rng, Q& q)
 {
+    constexpr int CB = DqOf<G>::cb, XB = DqOf<G>::xb;
+    constexpr uint32_t CM = (1u << CB) - 1u, HM = (uint32_t)G::DQ - 1u;
     uint32_t hdr = q.get(0), e0, e1;
-    const uint32_t cnt = hdr & 7u, head = (hdr >> 3) & 3u;
+    const uint32_t cnt = hdr & CM, head = (hdr >> CB) & HM;
     if (cnt) {
         e0 = q.get(1 + 2 * head);
         e1 = q.get(2 + 2 * head);
-        hdr = (hdr & ~0x1Fu) | (cnt - 1u) | ((head + 1u) & (uint32_t)(G::DQ - 1)) << 3;
+        hdr = (hdr & ~((1u << XB) - 1u)) | (cnt - 1u) | ((head + 1u) & HM) << CB;
     } else {
         g.make_deal(rng, hdr, e0, e1);
     }
@@ -587,16 +593,21 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
     }
     // the deal queues of the wave's envs for the launch: in registers, or in LDS (DQW consecutive words per lane:
     // odd stride), per the game's DQ_REGS
+    // or in place in the env state in HBM (per the game's DQ_HBM: no copy, no LDS; lanes without an env never touch it)
     constexpr int DQ = DqOf<G>::value, DQW = DqOf<G>::words;
-    constexpr bool QREGS = DqOf<G>::regs;
-    __shared__ uint32_t dql[DQ > 0 && !QREGS ? WAVES_PER_BLOCK * G::EPW * DQW : 1];
+    constexpr bool QREGS = DqOf<G>::regs, QHBM = DqOf<G>::hbm;
+    __shared__ uint32_t dql[DQ > 0 && !QREGS && !QHBM ? WAVES_PER_BLOCK * G::EPW * DQW : 1];
     using QV = std::conditional_t<QREGS, DqRegs<DQW ? DQW : 1>, DqMem>;
     QV q{};
     if constexpr (DQ > 0) {
-        if constexpr (!QREGS) q = DqMem{dql + (c.wid * G::EPW + (c.lane < G::EPW ? c.lane : 0)) * DQW, 1};
-        if (c.valid) {
+        if constexpr (QHBM) {
+            q = DqMem{st + (int64_t)G::GW * n + (c.valid ? c.env : 0), n};
+        } else {
+            if constexpr (!QREGS) q = DqMem{dql + (c.wid * G::EPW + (c.lane < G::EPW ? c.lane : 0)) * DQW, 1};
+            if (c.valid) {
 #pragma unroll
-            for (int w = 0; w < DQW; w++) q.set(w, st[(int64_t)(G::GW + w) * n + c.env]);
+                for (int w = 0; w < DQW; w++) q.set(w, st[(int64_t)(G::GW + w) * n + c.env]);
+            }
         }
     }
     G g;
@@ -692,8 +703,9 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
 #endif
         if constexpr (DQ > 0) {
             // a lane ending its game with an empty queue makes every lane with room draw one deal ahead, in lockstep
-            if (__ballot(c.valid && done && (q.get(0) & 7u) == 0u)) {
-                if (c.valid && (q.get(0) & 7u) < (uint32_t)DQ) dq_push(g, m, q);
+            constexpr uint32_t CM = (1u << DqOf<G>::cb) - 1u;   // the header's count field
+            if (__ballot(c.valid && done && (q.get(0) & CM) == 0u)) {
+                if (c.valid && (q.get(0) & CM) < (uint32_t)DQ) dq_push(g, m, q);
             }
             if (c.valid && done) dq_reset(g, m, q);
         }
@@ -709,7 +721,7 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
     }
     if (c.valid) {
         g.store(st, n, c.env);
-        if constexpr (DQ > 0) {
+        if constexpr (DQ > 0 && !QHBM) {
 #pragma unroll
             for (int w = 0; w < DQW; w++) st[(int64_t)(G::GW + w) * n + c.env] = q.get(w);
         }

@@ -267,11 +267,13 @@ class VecEnv:
         gw = self.game_words
         if gw is not None and self.info.state_words > gw:
             w = self.env_state_words(env)
-            cap = (len(w) - gw - 1) // 2
+            cap = (len(w) - gw - 1) // 2                 # queue depth DQ (4 or 8)
+            cb = cap.bit_length()                         # header: count:cb, head:cb-1, 2 dealer bits, draws[8:7]
+            xb = 2 * cb - 1
             hdr = w[gw]
-            for k in range(hdr & 7):
-                slot = (((hdr >> 3) & 3) + k) % cap
-                pos -= ((w[gw + 1 + 2 * slot] >> 25) & 127) | ((hdr >> (7 + 2 * slot)) & 3) << 7
+            for k in range(hdr & ((1 << cb) - 1)):
+                slot = (((hdr >> cb) & (cap - 1)) + k) % cap
+                pos -= ((w[gw + 1 + 2 * slot] >> 25) & 127) | ((hdr >> (xb + 2 + 2 * slot)) & 3) << 7
         return pos % self.rng_period
 
     def set_kernel_flags(self, flags):
