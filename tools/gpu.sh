@@ -62,7 +62,7 @@ for step in "$@"; do
       python3 tools/pmc_summary.py "$d" > "$d/summary.txt" 2>&1; cat "$d/summary.txt" ;;
     profile)
       g=${a[1]}; extra=$(echo "${a[*]:2}" | tr ',' ' '); d=$O/prof_$g; mkdir -p "$d"
-      B="bench.py --game $g --no-cpu-baseline --no-philox --placement 0 --gather none --steps ${STEPS:-100} $extra"
+      B="bench.py --game $g --no-cpu-baseline --no-philox --no-device-state --placement 0 --gather none --steps ${STEPS:-100} $extra"   # no amd-smi child: under rocprofv3 its env -> python3 hop is an exec after GPU init
       run 300 "$d/bench_kt.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$d/kt" -o kt -- python3 $B
       run 300 "$d/bench_fetch.log" rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$d/fetch" -o fetch -- python3 $B
       run 300 "$d/bench_write.log" rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$d/write" -o write -- python3 $B
