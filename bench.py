@@ -29,23 +29,28 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md (chip-level parameters)
 MT_N = 624              # words per MT19937 block
 
-# per game: default envs per GPU (BASELINE.json configs), default fused steps per launch, packed state bytes per env
-# read + written once per launch (state words + the RNG control word; hold'em: 4 game words + the 8-deal queue), the expected tempered-u32 MT19937 draws per
-# env-step under random play (exact acceptance rates of random_interval x random-play game lengths). The
+# per game: default envs per GPU (BASELINE.json configs), default fused steps per launch, the expected tempered-u32
+# MT19937 draws per env-step under random play (exact acceptance rates of random_interval x random-play game lengths). The
 # stream geometry (draws before the first refill, draws per refill) comes from the built library (VecEnv.rng_period:
 # the byte ring's CS_RING_SLOTS, or DouDizhu's two-block word window), see precondition_launches.
 # Fused steps per launch, measured on one box: Leduc 256 vs 128 +3 % (T >= 256), 512 vs 256 -9 %;
 # Limit / No-limit 512 vs 256 +1.5 % (round 3; 256 vs 128 +1.5 / +2 %), DouDizhu 128 vs 64 -5 %, 32 vs 64 -2 % (two-env
 # kernel), Blackjack 128 vs 64 +2 %.
 GAMES = {
-    'leduc-holdem': dict(envs=1 << 20, T=256, state_bytes=2 * 4 + 4, draws_per_step=2.83),
-    'limit-holdem': dict(envs=262144, T=512, state_bytes=21 * 4 + 4, draws_per_step=24.5),
-    'blackjack': dict(envs=1 << 20, T=128, state_bytes=20 * 4 + 4, draws_per_step=57.0),
-    'doudizhu': dict(envs=65536, T=64, state_bytes=36 * 4 + 4, draws_per_step=1.21),
+    'leduc-holdem': dict(envs=1 << 20, T=256, draws_per_step=2.83),
+    'limit-holdem': dict(envs=262144, T=512, draws_per_step=24.5),
+    'blackjack': dict(envs=1 << 20, T=128, draws_per_step=57.0),
+    'doudizhu': dict(envs=65536, T=64, draws_per_step=1.21),
     # not a BASELINE config; draws/step counted on the oracle (4096 envs x 256 random steps)
-    'no-limit-holdem': dict(envs=262144, T=512, state_bytes=21 * 4 + 4, draws_per_step=26.3),
+    'no-limit-holdem': dict(envs=262144, T=512, draws_per_step=26.3),
 }
 TIMED_TARGET_S = 2.0     # default --steps: enough launches for >= ~2 s of timed region (box variance, SMI sampler)
+
+
+def state_bytes(info):
+    """Packed state bytes per env read + written once per launch: the built library's state words (hold'em: the game
+    words + the deal queue, whatever depth was compiled) + the RNG control word."""
+    return 4 * info.state_words + 4
 
 
 def alg_bytes_per_env_step(info, T, game):
@@ -54,7 +59,7 @@ def alg_bytes_per_env_step(info, T, game):
     g = GAMES[game]
     a = 1 if info.num_actions <= 256 else 2
     return (info.obs_dim + (info.num_actions + 7) // 8 + 4 * info.num_players + 1 + 1 + a
-            + 2.0 * g['state_bytes'] / T + 8.0 * g['draws_per_step'])
+            + 2.0 * state_bytes(info) / T + 8.0 * g['draws_per_step'])
 
 
 def alg_bytes_philox(info, T, game):
@@ -82,18 +87,33 @@ def kernel_source_digest():
     return h.hexdigest()[:16]
 
 
-def measured_traffic(game, envs, T):
-    """HBM bytes per k_rollout launch of this configuration from the committed rocprofv3 PMC profile
-    (profiles/traffic.json, written by tools/pmc_traffic.py), or None. An entry measured on other kernel sources
-    is returned with stale=True and is not used as `traffic`."""
+def measured_traffic(game, envs, T, kernel_ms=None):
+    """HBM bytes per k_rollout launch of this configuration from the committed rocprofv3 profiles
+    (profiles/traffic.json, written by tools/pmc_traffic.py), or None. An entry is one profile or a list of them
+    (one per HBM placement class); the one measured on these kernel sources whose kernel time is closest to
+    `kernel_ms` is returned. Entries measured on other kernel sources are returned with stale=True and are not used
+    as `traffic`."""
     try:
         with open(os.path.join(ROOT, 'profiles', 'traffic.json')) as f:
             e = json.load(f).get('%s:%d:%d' % (game, envs, T))
     except (OSError, ValueError):
         return None
-    if e is not None:
-        e = dict(e, stale=e.get('src_sha16') != kernel_source_digest())
-    return e
+    if e is None:
+        return None
+    digest = kernel_source_digest()
+    es = [dict(x, stale=x.get('src_sha16') != digest) for x in (e if isinstance(e, list) else [e])]
+    fresh = [x for x in es if not x['stale']] or es
+    if kernel_ms is not None:
+        fresh.sort(key=lambda x: abs(x.get('kernel_ns_timed_mean', 0) / 1e6 - kernel_ms))
+    return fresh[0]
+
+
+def under_profiler():
+    """True when a profiler's library is preloaded into this process (rocprofv3 sets LD_PRELOAD / ROCPROF_*): then
+    no child process may be started from here -- the amd-smi sampler's `env -> python3` hop would be an exec after
+    the preloaded library initialised the GPU."""
+    pre = os.environ.get('LD_PRELOAD', '')
+    return 'rocprof' in pre or 'roctracer' in pre or any(k.startswith(('ROCPROF', 'ROCP_')) for k in os.environ)
 
 
 def _cpu_worker(game, first, n, T, budget_s, q):
@@ -188,9 +208,13 @@ def main():
     ap.add_argument('--placement', type=int, default=3,
                     help='N=1: time a few launches into this many fresh trajectory allocations after the timed region '
                          '(untimed context under "placement"; 0: off)')
-    ap.add_argument('--no-device-state', dest='device_state', action='store_false',
-                    help='skip the amd-smi / HIP attribute sample of the box (reported under "device")')
+    ap.add_argument('--device-state', dest='device_state', action='store_true', default=None,
+                    help='sample the box (HIP attributes + amd-smi, reported under "device"); default: on, except '
+                         'under a profiler (no child processes there)')
+    ap.add_argument('--no-device-state', dest='device_state', action='store_false')
     args = ap.parse_args()
+    if args.device_state is None:
+        args.device_state = not under_profiler()
 
     import torch
     import torch.distributed as dist
@@ -206,6 +230,22 @@ def main():
     if world > 1:
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
+
+    # the box's state: HIP attributes + amd-smi's clocks / partition modes, queried by a host
+    # thread while the envs are built and preconditioned, joined BEFORE the timed region (so even a 20-launch driver
+    # run records it and the queries never overlap the timed launches)
+    import threading
+    dev_state, dev_state_lock = {}, threading.Lock()
+    state_thread = None
+    if rank == 0 and args.device_state:
+        from tools.device_state import device_state
+
+        def sample_state():
+            d = device_state(local)
+            with dev_state_lock:
+                dev_state.update(d)
+        state_thread = threading.Thread(target=sample_state, daemon=True)
+        state_thread.start()
 
     def barrier():
         if world > 1:
@@ -236,23 +276,24 @@ def main():
         steps = int(min(4000, max(20, math.ceil(TIMED_TARGET_S / max(per, 1e-6)))))
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-    dev_state, pw = {}, None
+    pw = None
+    state_snapshot = {}
+    if state_thread is not None:
+        state_thread.join(timeout=90)   # device_state's amd-smi queries are bounded at 25 + 25 + 15 s
+        with dev_state_lock:
+            state_snapshot = dict(dev_state) if not state_thread.is_alive() else {}
     if rank == 0 and args.device_state:
-        # the box's state while the timed launches run (boxes run the same kernel at 3.5 or
-        # 4.3 ms): HIP attributes + amd-smi's clocks / partition modes (a host thread), and the power window --
-        # average power, package-power-limit (PPT) residency, XCD clocks -- from in-process gpu_metrics reads
-        import threading
-        from tools.device_state import device_state, PowerWindow
+        # the power window over the timed launches -- average power, package-power-limit (PPT) residency, XCD clocks
+        # -- from in-process gpu_metrics reads (sysfs through the amdsmi library: no child process), sampled every
+        # 20 ms so that even a short timed region gets clock samples
+        from tools.device_state import PowerWindow
         pw = PowerWindow(local)
-
         stop_sampling = threading.Event()
 
         def sample():
-            t_state = time.perf_counter() + 0.5
-            while not stop_sampling.wait(0.1):
+            pw.mid()
+            while not stop_sampling.wait(0.02):
                 pw.mid()
-                if not dev_state and time.perf_counter() >= t_state:
-                    dev_state.update(device_state(local))
         sampler = threading.Thread(target=sample, daemon=True)
     barrier()
     torch.cuda.synchronize()
@@ -273,8 +314,8 @@ def main():
     barrier()
     elapsed = rank_max(time.perf_counter() - t0, dev)
     kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
-    if rank == 0 and args.device_state:
-        sampler.join(timeout=60)   # the amd-smi query may outlast a short timed region
+    if pw is not None:
+        sampler.join(timeout=5)
 
     placement = None
     if world == 1 and args.placement > 0:
@@ -373,19 +414,27 @@ def main():
                          'alg_bytes_per_env_step': B, 'alg_bytes_per_launch': B * N * T,
                          'kernel_ms_per_launch': kernel_ms, 'kernel': 'k_rollout<%s>' % game},
         }
-        tr = measured_traffic(game, N, T)
+        tr = measured_traffic(game, N, T, kernel_ms)
         if tr is not None:   # per launch, like `achieved`; from the profile of this exact configuration and kernels
             if tr['stale']:
                 line['roofline']['traffic_stale'] = '%s measured other kernel sources' % tr['source']
             else:
                 line['roofline']['traffic'] = tr['bytes_per_launch']
                 line['roofline']['traffic_source'] = tr['source']
-        if dev_state or power:
-            smi = dev_state.get('smi') or {}
+                # the cited profile's own kernel time (rocprofv3 kernel trace of its timed launches) next to this
+                # line's HIP-event time: a profile is evidence for the line only if they agree
+                pk = tr.get('kernel_ns_timed_mean')
+                if pk:
+                    pk = pk / 1e6
+                    line['roofline']['profile_kernel_ms'] = pk
+                    line['roofline']['profile_frac'] = B * N * T / (pk * 1e-3) / 1e9 / HBM_PEAK_GBS
+                    line['roofline']['profile_mismatch'] = abs(pk - kernel_ms) > 0.05 * kernel_ms
+        if state_snapshot or power:
+            smi = state_snapshot.get('smi') or {}
             keep = ('bus', 'gfx_0_mhz', 'gfx_0_max_mhz', 'mem_0_mhz', 'fclk_0_mhz', 'power_w', 'power_cap_static',
                     'temp_hotspot', 'temp_mem', 'driver')
-            line['device'] = dict(name=dev_state.get('name'), arch=dev_state.get('arch'), hip=dev_state.get('hip'),
-                                  smi={k: smi.get(k) for k in keep},
+            line['device'] = dict(name=state_snapshot.get('name'), arch=state_snapshot.get('arch'),
+                                  hip=state_snapshot.get('hip'), smi={k: smi.get(k) for k in keep},
                                   partition=(smi.get('partition') or {}).get('current_partition'),
                                   timed_window=power)
         if placement is not None:

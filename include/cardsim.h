@@ -59,6 +59,11 @@ typedef struct {
     int32_t action_feature_dim; /* bytes per cs_action_features row: doudizhu 54, otherwise num_actions (one-hot) */
     int32_t rng_period;   /* draws after which the stream position of cs_get_rng_ctl wraps: doudizhu 1 248 (two word
                              blocks), the others the byte ring's 9 984 (16 slots of 624) */
+    int32_t game_words;   /* packed game words at the start of the state_words (cs_get_env_state); = state_words for
+                             every game without a deal queue */
+    int32_t deal_queue_depth; /* DQ: deals the rollout may draw ahead (heads-up Limit / No-limit hold'em: 8 in this
+                             build; 0 = no queue). state_words = game_words + 1 + 2 * DQ when DQ > 0; layout at
+                             cs_get_env_state */
 } cs_game_info;
 
 /* Outputs of reset/step/observe, all device pointers, one row per env:
@@ -222,10 +227,19 @@ int cs_dmc_select(const float* values, const int32_t* counts, const int64_t* off
                   float eps, uint64_t seed, uint64_t t, uint64_t state_base, int32_t* actions, void* stream);
 
 /* Copy the packed state words of env `env` (state_words u32, HOST buffer) -- the raw fields behind
- * Env.get_state()['raw_obs'] / get_perfect_information for single-env compatibility and debugging. Limit and
- * No-limit hold'em: 4 game words, then the env's deal queue (deals the rollout drew ahead from the stream; a header
- * word -- count in bits 0..2, head in 3..4 -- and 4 entries of two words, e0 bits 25..31 + header bits 7 + 2 slot ..
- * 8 + 2 slot = MT draws of the entry). Synchronous. */
+ * Env.get_state()['raw_obs'] / get_perfect_information for single-env compatibility and debugging. Synchronous.
+ * Heads-up Limit and No-limit hold'em (cs_game_info.deal_queue_depth = DQ > 0): words [0, game_words) are the game,
+ * then the env's deal queue -- deals the rollout drew ahead from the env's stream, oldest first, that the next games
+ * will use -- as one header word H and DQ entries of two words (entry k at words game_words + 1 + 2k, +2 + 2k). With
+ * CB = log2(DQ) + 1 and XB = 2 CB - 1 (DQ 8: CB 4, XB 7; DQ 4: CB 3, XB 5):
+ *   H bits [0, CB)        number of queued deals (0..DQ)
+ *   H bits [CB, 2CB - 1)  slot of the oldest queued deal; queued deal i (i < count) is in slot (head + i) % DQ
+ *   H bit XB, XB + 1      No-limit only: the dealer seat has been drawn / the drawn dealer seat
+ *   H bits XB + 2 + 2k, XB + 3 + 2k   bits 8..7 of slot k's draw count
+ *   e0 (first word of a slot) bits 25..31  bits 6..0 of the slot's draw count: MT19937 words the deal consumed
+ *                                          (saturating at 511), so the env's position in its own game stream is the
+ *                                          cs_get_rng_ctl position minus the queued deals' draw counts
+ * Other bits of the entries are the engine's packed deal (holes, board, blind seat) -- opaque to a consumer. */
 int cs_get_env_state(cs_handle* h, int64_t env, uint32_t* host_words, int32_t nwords);
 
 /* Asynchronous cs_get_env_state: the state words of env `env` copied on `stream` into dst (u32 [state_words],
@@ -257,7 +271,9 @@ int cs_copy_env_rng(cs_handle* h, int64_t env, uint32_t* dst, void* stream);
 int cs_load_env_rng(cs_handle* h, int64_t env, const uint32_t* src, void* stream);
 
 /* Stream position (u32 draws consumed) bookkeeping word of env `env` (HOST out). Synchronous; for parity tests.
- * Hold'em envs: the position includes the draws of the queued deals (see cs_get_env_state). */
+ * The position is ctl & 0x3FFF (DouDizhu: ctl & 0x7FF), the draws consumed modulo cs_game_info.rng_period; the other
+ * bits are the engine's. Hold'em envs with a deal queue: the position includes the draws of the queued deals (their
+ * counts are decoded as cs_get_env_state documents; tools/abi_driver.c). */
 int cs_get_rng_ctl(cs_handle* h, int64_t env, uint32_t* host_ctl);
 
 /* Evaluator test hook: the value the hold'em kernels' showdown evaluator gives `n` 7-card hands (Hand.evaluateHand +

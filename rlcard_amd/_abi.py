@@ -25,7 +25,8 @@ RNG_MODES = {'mt19937': 0, 'philox': 1}   # cs_config.rng_mode
 class GameInfo(C.Structure):
     _fields_ = [('obs_dim', C.c_int32), ('num_actions', C.c_int32), ('num_players', C.c_int32),
                 ('legal_bytes', C.c_int32), ('action_bytes', C.c_int32), ('state_words', C.c_int32),
-                ('action_feature_dim', C.c_int32), ('rng_period', C.c_int32)]
+                ('action_feature_dim', C.c_int32), ('rng_period', C.c_int32), ('game_words', C.c_int32),
+                ('deal_queue_depth', C.c_int32)]
 
 
 class StepOut(C.Structure):

@@ -405,6 +405,7 @@ int bjs_game_info(const cs_config* cfg, cs_game_info* info)
     info->state_words = bjs::WORDS;
     info->action_feature_dim = 2;
     info->rng_period = MT_N;   // position = words consumed of the current 624-word block
+    info->game_words = bjs::WORDS;
     return CS_OK;
 }
 

@@ -1253,6 +1253,12 @@ struct PairArgs {
     int32_t T, kfl;
 };
 typedef const __attribute__((address_space(4))) PairArgs* PairArgsK;
+// read back through __builtin_amdgcn_kernarg_segment_ptr() (RolloutArgs, cs_skeleton.h): PairArgs must stay
+// k_rollout2's ONLY explicit parameter; any new argument goes inside the struct
+static_assert(std::is_standard_layout<PairArgs>::value && std::is_trivially_copyable<PairArgs>::value,
+              "PairArgs is copied into the kernarg segment bytewise");
+static_assert(offsetof(PairArgs, mt) == 0 && alignof(PairArgs) == 8 && sizeof(PairArgs) % 8 == 0,
+              "PairArgs: first kernarg at offset 0, 8-byte aligned");
 
 template <bool PHX>
 __global__ __launch_bounds__(PBLOCK, CS_DDZ_PAIR_MINW) void k_rollout2(PairArgs args)

@@ -66,6 +66,7 @@ int game_info(int32_t game, const cs_config* cfg, cs_game_info* info)
         info->state_words = ddz::WORDS;
         info->action_feature_dim = 54;
         info->rng_period = 2 * 624;
+        info->game_words = ddz::WORDS;
         return CS_OK;
     default:
         return CS_E_UNSUPPORTED;

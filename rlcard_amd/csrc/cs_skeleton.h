@@ -4,6 +4,7 @@
 // instantiate games (cs_kernels.hip: the heads-up / single-table games; cs_holdem_n.hip: 3..6-player hold'em).
 // Integer/branchy work: no MFMA. The bound is HBM (obs/legal/reward rows out, packed state + RNG words in/out).
 #pragma once
+#include <cstddef>
 #include <type_traits>
 
 #include "cs_device.h"
@@ -58,7 +59,7 @@ __device__ __forceinline__ LaneCtx lane_ctx(int64_t n)
 {
     LaneCtx c;
     c.lane = threadIdx.x & (WAVE - 1);
-    c.wid = threadIdx.x / WAVE;
+    c.wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // wave-uniform: wave_first lives in SGPRs
     c.wave_first = ((int64_t)blockIdx.x * WAVES_PER_BLOCK + c.wid) * EPW;
     c.env = c.wave_first + c.lane;
     const int64_t left = n - c.wave_first;
@@ -130,6 +131,32 @@ template <class G, class = void>
 struct SparseObs : std::false_type {};
 template <class G>
 struct SparseObs<G, std::void_t<decltype(G::SPARSE_K)>> : std::bool_constant<(G::SPARSE_K > 0)> {};
+template <class G, class = void>
+struct SparseK {   // positions per sparse row (1 where the game has none: a placeholder array)
+    static constexpr int value = 1;
+};
+template <class G>
+struct SparseK<G, std::void_t<decltype(G::SPARSE_K)>> {
+    static constexpr int value = G::SPARSE_K > 0 ? G::SPARSE_K : 1;
+};
+
+// k_rollout's order inside a step, per game (G::STORES_LAST, default 0; CS_STORES_LAST = 0 / 1 overrides every game
+// for A/B builds): 1 = every trajectory store of the step after its refill / restage loads -- on gfx950 one counter
+// (vmcnt) tracks loads and stores in issue order, so a load issued after the rows waits until every row store is
+// acknowledged, a drain whose length is the HBM write latency of the moment, which depends on where the trajectory
+// landed in HBM (Leduc 4.05 -> 4.02 ms on torch allocations, 5.1 -> 4.1 on physically contiguous
+// ones); 0 = each row stored where it is produced (Limit: 8.1 vs 8.35 ms -- VALU-bound, the rows' live ranges cost more)
+#ifndef CS_STORES_LAST
+#define CS_STORES_LAST -1
+#endif
+template <class G, class = void>
+struct StoresLast {
+    static constexpr bool value = CS_STORES_LAST == 1;
+};
+template <class G>
+struct StoresLast<G, std::void_t<decltype(G::STORES_LAST)>> {
+    static constexpr bool value = CS_STORES_LAST >= 0 ? CS_STORES_LAST == 1 : G::STORES_LAST;
+};
 
 template <class G>
 __device__ __forceinline__ void emit_legal(uint8_t* legal, int64_t row, uint64_t lg)
@@ -552,6 +579,13 @@ struct RolloutArgs {
     int32_t T, flags;
 };
 typedef const __attribute__((address_space(4))) RolloutArgs* RolloutArgsK;
+// k_rollout reads its argument back through __builtin_amdgcn_kernarg_segment_ptr(), so RolloutArgs must stay the
+// kernel's ONLY explicit parameter (then it sits at kernarg offset 0 with exactly the host layout): any new argument
+// goes inside the struct
+static_assert(std::is_standard_layout<RolloutArgs>::value && std::is_trivially_copyable<RolloutArgs>::value,
+              "RolloutArgs is copied into the kernarg segment bytewise");
+static_assert(offsetof(RolloutArgs, mt) == 0 && alignof(RolloutArgs) == 8 && sizeof(RolloutArgs) % 8 == 0,
+              "RolloutArgs: first kernarg at offset 0, 8-byte aligned");
 
 template <class G>
 __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs args)
@@ -573,6 +607,7 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
     __shared__ __attribute__((aligned(16))) uint8_t stage[WAVES_PER_BLOCK][StageBytes<G>::value];
     const LaneCtx c = lane_ctx<G::EPW>(n);
     RingLane<G::STAGE_MODE> m = ring_lane<G::STAGE_MODE>(mt, ctl, c);
+    constexpr bool SL = StoresLast<G>::value;
     // MT staging needs both blocks valid at every restage, i.e. the cooperative refill (flag bit 0 off);
     // flag bit 1 disables it (one global load per draw) for A/B runs and fallback-path tests
     const bool staged = !(flags & 3);
@@ -622,10 +657,19 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
     }
     refill<G>(m, c.lane, flags & 1);
     if (staged) restage<G>(m, stage[c.wid], c.lane, c.valid);
-    const uint64_t genv = args.env_base + (uint64_t)c.env;
     PolicyRng pol;
     for (int t = 0; t < T; t++) {
         const RolloutArgs& A = arg();
+        // the lane id made opaque at every step, so lane-derived values (env id, row and LDS addresses) are recomputed
+        // from it instead of held across the step -- at 6 waves per SIMD (80 VGPRs) the held copies were spilled, and
+        // a spill reload waits on every store the wave has in flight (vmcnt)
+        LaneCtx cl = c;
+        {
+            int ol = c.lane;
+            asm volatile("" : "+v"(ol));
+            cl.lane = ol;
+            cl.env = c.wave_first + ol;
+        }
         const cs_traj_out& out = A.out;
         uint8_t* obs = (uint8_t*)out.obs;
         uint8_t* legal = (uint8_t*)out.legal;
@@ -639,21 +683,45 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
         const uint64_t lg = g.legal();
         uint32_t bits[G::NB];
         g.observe(p, bits);
+        // the policy counter's env id from scalars + the lane id at each step (a loop-invariant 64-bit value would be
+        // one more pair of VGPRs held across the step -- spilled, and its reload waits on the step's stores)
+        const uint64_t genv = A.env_base + (uint64_t)(c.wave_first + cl.lane);
         const uint32_t pr = pol.at(seed, genv, t0 + (uint64_t)t, t == 0);
         int a;
         if constexpr (G::A <= 8) a = pick_legal_small<G::A>((uint32_t)lg, pr);
         else a = G::A <= 32 ? pick_legal32((uint32_t)lg, pr) : pick_legal(lg, pr);
-#ifndef CS_PROF_NO_OBS   // profiling builds only (tools: make variant DEFS=-DCS_PROF_NO_OBS): outputs incomplete
-        if constexpr (SparseObs<G>::value) {   // one-hot rows with a few known positions (row_write_sparse)
-            uint32_t pos[G::SPARSE_K];
-            const uint32_t tail = g.observe_pos(p, pos);
-            row_write_sparse<G::OBS, G::EPW, G::SPARSE_K, G::RAW_OBS>(lds[c.wid], pos,
-                                                                      obs + (rowbase + c.wave_first) * G::OBS, c.lane,
-                                                                      c.nvalid, !(flags & 4), tail);
-        } else {
-            emit_obs<G, G::EPW>(lds[c.wid], bits, obs, rowbase + c.wave_first, flags, c);
+        constexpr int SK = SparseK<G>::value, SKW = (SK + 3) / 4;
+        uint32_t pos[SK];
+        uint32_t tail = 0;
+        if constexpr (SparseObs<G>::value) tail = g.observe_pos(p, pos);   // the pre-step view's one-hot positions
+        // with the stores after the step's loads, the view lives across the step, the refill and the restage: its
+        // positions (< 256) packed four per word, made opaque so the compiler keeps the packed form, not the array
+        uint32_t posw[SKW];
+        if constexpr (SparseObs<G>::value && SL) {
+            static_assert(G::OBS <= 256, "positions packed as bytes");
+#pragma unroll
+            for (int w = 0; w < SKW; w++) {
+                posw[w] = 0;
+#pragma unroll
+                for (int k = 4 * w; k < 4 * w + 4 && k < SK; k++) posw[w] |= pos[k] << (8 * (k - 4 * w));
+                asm volatile("" : "+v"(posw[w]));
+            }
         }
+        auto store_obs = [&]() {
+#ifndef CS_PROF_NO_OBS   // profiling builds only (tools: make variant DEFS=-DCS_PROF_NO_OBS): outputs incomplete
+            if constexpr (SparseObs<G>::value) {   // one-hot rows with a few known positions (row_write_sparse)
+                if constexpr (SL) {
+#pragma unroll
+                    for (int k = 0; k < SK; k++) pos[k] = (posw[k / 4] >> (8 * (k % 4))) & 255u;
+                }
+                row_write_sparse<G::OBS, G::EPW, SK, G::RAW_OBS>(
+                    lds[c.wid], pos, obs + (rowbase + c.wave_first) * G::OBS, cl.lane, c.nvalid, !(flags & 4), tail);
+            } else {
+                emit_obs<G, G::EPW>(lds[c.wid], bits, obs, rowbase + c.wave_first, flags, cl);
+            }
 #endif
+        };
+        if constexpr (!SL) store_obs();
         // the reward row starts from a zero the compiler cannot hoist out of the loop: a loop-invariant zero pair was
         // kept in a scratch spill whose reload, before each step's reward store, waited on vmcnt(0) -- on gfx950 every
         // store the wave had issued (the obs rows): a drain per step
@@ -666,14 +734,33 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
 #pragma unroll
         for (int k = 0; k < G::P; k++) r[k] = __uint_as_float(zr);
         bool done = false;
-        if (c.valid) {
-            const int64_t row = rowbase + c.env;
+        const int64_t row = rowbase + cl.env;
+        // legal mask, player and action of the pre-step view, one word while they wait for the stores (A <= 16)
+        constexpr bool PACK_SMALL = SL && G::A <= 16 && G::ACTION_BYTES == 1;
+        uint32_t pre = 0;
+        if constexpr (PACK_SMALL) {
+            pre = (uint32_t)lg | (uint32_t)p << 16 | ((uint32_t)a & 255u) << 24;
+            asm volatile("" : "+v"(pre));
+        }
+        auto store_small_pre = [&]() {   // legal, player, action: the pre-step view and the action taken
+            const uint64_t lg_ = PACK_SMALL ? (uint64_t)(pre & 0xFFFFu) : lg;
+            const int p_ = PACK_SMALL ? (int)((pre >> 16) & 255u) : p;
+            const int a_ = PACK_SMALL ? (int)(int8_t)(pre >> 24) : a;
 #ifndef CS_PROF_NO_SMALL
-            emit_legal<G>(legal, row, lg);
-            out_store(player + row, (uint8_t)p);
+            emit_legal<G>(legal, row, lg_);
+            out_store(player + row, (uint8_t)p_);
 #endif
-            if constexpr (G::ACTION_BYTES == 1) out_store((uint8_t*)out.action + row, (uint8_t)a);
-            else out_store((int16_t*)out.action + row, (int16_t)a);
+            if constexpr (G::ACTION_BYTES == 1) out_store((uint8_t*)out.action + row, (uint8_t)a_);
+            else out_store((int16_t*)out.action + row, (int16_t)a_);
+        };
+        auto store_small_post = [&]() {   // reward, done: the transition's outcome
+#ifndef CS_PROF_NO_SMALL
+            if constexpr (!RewardPairs<G>::value) emit_reward<G>(reward, row, r);
+            out_store(done_o + row, (uint8_t)done);
+#endif
+        };
+        if (c.valid) {
+            if constexpr (!SL) store_small_pre();
             g.step(a, m);
             done = g.is_over();
             if (done) {
@@ -687,20 +774,20 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
                     }
                 }
             }
-#ifndef CS_PROF_NO_SMALL
-            if constexpr (!RewardPairs<G>::value) emit_reward<G>(reward, row, r);
-            out_store(done_o + row, (uint8_t)done);
-#endif
+            if constexpr (!SL) store_small_post();
             if constexpr (DQ == 0) {
                 if (done) g.reset(m);
             }
         }
+        auto store_reward_pairs = [&]() {
 #ifndef CS_PROF_NO_SMALL
-        if constexpr (RewardPairs<G>::value) {
-            if constexpr (CS_REWARD_PAIRS == 2) emit_reward_t<G::EPW>(reward, rowbase, r, c);
-            else emit_reward_pairs(reward, rowbase, r, c);
-        }
+            if constexpr (RewardPairs<G>::value) {
+                if constexpr (CS_REWARD_PAIRS == 2) emit_reward_t<G::EPW>(reward, rowbase, r, c);
+                else emit_reward_pairs(reward, rowbase, r, c);
+            }
 #endif
+        };
+        if constexpr (!SL) store_reward_pairs();
         if constexpr (DQ > 0) {
             // a lane ending its game with an empty queue makes every lane with room draw one deal ahead, in lockstep
             constexpr uint32_t CM = (1u << DqOf<G>::cb) - 1u;   // the header's count field
@@ -709,8 +796,19 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
             }
             if (c.valid && done) dq_reset(g, m, q);
         }
-        refill<G>(m, c.lane, flags & 1);
-        if (staged) restage<G>(m, stage[c.wid], c.lane, c.valid);
+        refill<G>(m, cl.lane, flags & 1);
+        if (staged) restage<G>(m, stage[c.wid], cl.lane, c.valid);
+        if constexpr (SL) {
+            // the step's rows leave after the step's loads (refill, restage): on gfx950 one counter (vmcnt) tracks
+            // loads and stores in issue order, so a load issued after the rows waits until every row store is
+            // acknowledged -- a drain whose length is the HBM write latency of the moment
+            store_obs();
+            if (c.valid) {
+                store_small_pre();
+                store_small_post();
+            }
+            store_reward_pairs();
+        }
     }
     bool keep = false;
     if constexpr (persist) {
@@ -789,6 +887,8 @@ static void fill_info(cs_game_info* info)
     info->state_words = G::WORDS;
     info->action_feature_dim = G::A;
     info->rng_period = (int32_t)RING;
+    info->deal_queue_depth = DqOf<G>::value;
+    info->game_words = G::WORDS - DqOf<G>::words;
 }
 
 template <class G>

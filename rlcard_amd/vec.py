@@ -246,28 +246,26 @@ class VecEnv:
 
     # heads-up hold'em games keep a deal queue after their 4 game words (rlcard_amd/csrc/cs_limit.h): deals drawn
     # ahead. 3..6-player hold'em has none (its judge may draw from the stream at a game's end, cs_holdem_n.h).
-    GAME_WORDS = {'limit-holdem': 4, 'no-limit-holdem': 4}
-
     @property
     def game_words(self):
-        """Packed game words before the deal queue, None when the game has no queue."""
-        return self.GAME_WORDS.get(self.env_id) if self.num_players == 2 else None
+        """Packed game words before the deal queue (cs_game_info.game_words), None when the game has no queue."""
+        return self.info.game_words if self.info.deal_queue_depth > 0 else None
 
     def game_state_words(self, env):
         """The packed game words of env `env` (without the hold'em deal queue)."""
-        gw = self.game_words
-        return self.env_state_words(env)[:gw if gw is not None else self.info.state_words]
+        return self.env_state_words(env)[:self.info.game_words]
 
     def rng_position(self, env):
         """Draws consumed by env `env`, modulo rng_period. Deals already drawn into a hold'em env's deal queue
-        do not count: they belong to the games after the current one."""
+        do not count: they belong to the games after the current one (queue layout: include/cardsim.h,
+        cs_get_env_state)."""
         v = C.c_uint32()
         _abi.check(_abi.lib().cs_get_rng_ctl(self._h, int(env), C.byref(v)), 'cs_get_rng_ctl')
         pos = v.value & (0x7FF if self.env_id == 'doudizhu' else 0x3FFF)   # cs_ring.h ctl layout
-        gw = self.game_words
-        if gw is not None and self.info.state_words > gw:
+        cap = self.info.deal_queue_depth
+        if cap > 0:
+            gw = self.info.game_words
             w = self.env_state_words(env)
-            cap = (len(w) - gw - 1) // 2                 # queue depth DQ (4 or 8)
             cb = cap.bit_length()                         # header: count:cb, head:cb-1, 2 dealer bits, draws[8:7]
             xb = 2 * cb - 1
             hdr = w[gw]

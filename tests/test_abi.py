@@ -75,3 +75,26 @@ def test_nplayer_game_info():
             _abi.game_info(game, top + 1)
     info, _ = _abi.game_info('no-limit-holdem', 6, chips_for_each=50, dealer_id=5)
     assert info.num_players == 6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('game', [1, 2, 4])   # Leduc, Limit, No-limit (the last two keep a deal queue)
+def test_c_driver_parity_and_deal_queue_decode(game):
+    """tools/abi_driver (C, no Python): a rollout through the ABI against the oracle, then every checked env's stream
+    position from cs_get_rng_ctl minus its queued deals' draws, decoded from cs_get_env_state with nothing but the
+    layout include/cardsim.h documents (game_words, deal_queue_depth, header bit fields), against the oracle."""
+    import subprocess
+    import sys
+    drv = os.path.join(ROOT, 'tools', 'abi_driver')
+    assert os.path.exists(drv), 'build() compiles tools/abi_driver'
+    n, T = 4096, 64
+    keys = subprocess.run([sys.executable, os.path.join(ROOT, 'tools', 'keys.py'), '42', str(n)], cwd=ROOT,
+                          capture_output=True, check=True).stdout
+    p = subprocess.run([drv, str(game), str(n), str(T), '1024'], input=keys, capture_output=True, cwd=ROOT,
+                       timeout=120)
+    out = p.stdout.decode()
+    assert p.returncode == 0, out + p.stderr.decode()
+    assert 'parity: 0 mismatching' in out and 'stream positions: 0 mismatching' in out, out
+    if game in (2, 4):
+        assert 'deal queue depth 8' in out
+        assert ' 0 of 1024 envs hold queued deals' not in out   # the decode was exercised

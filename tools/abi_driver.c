@@ -14,6 +14,25 @@
 #include "../include/cardsim.h"
 #include "../oracle/oracle.h"
 
+/* Draws that env's queued deals consumed, decoded from its cs_get_env_state words with nothing but the layout
+ * include/cardsim.h documents at cs_get_env_state (header word after game_words, CB = log2(DQ) + 1, XB = 2 CB - 1,
+ * per slot 7 low draw bits in e0 bits 25..31 and 2 high bits in the header at XB + 2 + 2 slot). */
+static uint32_t queued_draws(const uint32_t* w, const cs_game_info* info)
+{
+    const uint32_t dq = (uint32_t)info->deal_queue_depth;
+    if (dq == 0) return 0;
+    uint32_t cb = 1;
+    while ((1u << (cb - 1)) < dq) cb++;                 /* log2(DQ) + 1 */
+    const uint32_t xb = 2 * cb - 1, hdr = w[info->game_words];
+    const uint32_t count = hdr & ((1u << cb) - 1u), head = (hdr >> cb) & (dq - 1u);
+    uint32_t d = 0;
+    for (uint32_t i = 0; i < count; i++) {
+        const uint32_t slot = (head + i) % dq;
+        d += ((w[info->game_words + 1 + 2 * slot] >> 25) & 127u) | ((hdr >> (xb + 2 + 2 * slot)) & 3u) << 7;
+    }
+    return d;
+}
+
 #define CHECK(x)                                                                 \
     do {                                                                         \
         int rc_ = (x);                                                           \
@@ -80,21 +99,21 @@ int main(int argc, char** argv)
         if (hipMemcpy(host[k], dev[k], sz[k], hipMemcpyDeviceToHost) != hipSuccess) return 5;
     }
     /* oracle on the first W envs */
-    or_cfg oc = {info.num_players, 1};
+    or_cfg oc = {info.num_players, 1, 100, -1, 0};   /* the cs_config defaults: 1 deck, 100 chips, dealer drawn */
     or_batch* b = or_batch_create(game, W, &oc);
     or_batch_seed(b, keys, klen);
     size_t wr = (size_t)T * W;
-    uint8_t* eo = calloc(wr, info.obs_dim);
-    uint8_t* el = calloc(wr, info.legal_bytes);
-    uint8_t* ep = calloc(wr, 1);
-    int32_t* ea = calloc(wr, 4);
-    float* er = calloc(wr * info.num_players, 4);
-    uint8_t* ed = calloc(wr, 1);
-    uint8_t* tmp_o = calloc(W, info.obs_dim);
-    uint8_t* tmp_l = calloc(W, info.legal_bytes);
-    uint8_t* tmp_p = calloc(W, 1);
-    float* tmp_r = calloc(W * info.num_players, 4);
-    uint8_t* tmp_d = calloc(W, 1);
+    uint8_t* eo = (uint8_t*)calloc(wr, info.obs_dim);
+    uint8_t* el = (uint8_t*)calloc(wr, info.legal_bytes);
+    uint8_t* ep = (uint8_t*)calloc(wr, 1);
+    int32_t* ea = (int32_t*)calloc(wr, 4);
+    float* er = (float*)calloc(wr * info.num_players, 4);
+    uint8_t* ed = (uint8_t*)calloc(wr, 1);
+    uint8_t* tmp_o = (uint8_t*)calloc(W, info.obs_dim);
+    uint8_t* tmp_l = (uint8_t*)calloc(W, info.legal_bytes);
+    uint8_t* tmp_p = (uint8_t*)calloc(W, 1);
+    float* tmp_r = (float*)calloc(W * info.num_players, 4);
+    uint8_t* tmp_d = (uint8_t*)calloc(W, 1);
     or_batch_reset(b, tmp_o, tmp_l, tmp_p, tmp_r, tmp_d);
     or_batch_rollout(b, T, 5, 0, 0, eo, el, ep, ea, er, ed, NULL);
     long long bad = 0;
@@ -102,15 +121,48 @@ int main(int argc, char** argv)
         for (long long i = 0; i < W; i++) {
             size_t g = (size_t)t * n + i, e = (size_t)t * W + i;
             int a = info.action_bytes == 1 ? ((uint8_t*)host[3])[g] : ((int16_t*)host[3])[g];
-            if (memcmp((uint8_t*)host[0] + g * info.obs_dim, eo + e * info.obs_dim, info.obs_dim) ||
-                memcmp((uint8_t*)host[1] + g * info.legal_bytes, el + e * info.legal_bytes, info.legal_bytes) ||
-                ((uint8_t*)host[2])[g] != ep[e] || a != ea[e] || ((uint8_t*)host[5])[g] != ed[e] ||
-                memcmp((float*)host[4] + g * info.num_players, er + e * info.num_players, 4 * info.num_players)) {
-                if (bad < 5) fprintf(stderr, "mismatch t=%d env=%lld\n", t, i);
+            const char* what = NULL;
+            if (memcmp((uint8_t*)host[0] + g * info.obs_dim, eo + e * info.obs_dim, info.obs_dim)) what = "obs";
+            else if (memcmp((uint8_t*)host[1] + g * info.legal_bytes, el + e * info.legal_bytes, info.legal_bytes))
+                what = "legal";
+            else if (((uint8_t*)host[2])[g] != ep[e]) what = "player";
+            else if (a != ea[e]) what = "action";
+            else if (((uint8_t*)host[5])[g] != ed[e]) what = "done";
+            else
+                for (int k = 0; k < info.num_players; k++)   /* by value, as the Python tests (numpy) compare */
+                    if (((float*)host[4])[g * info.num_players + k] != er[e * info.num_players + k]) what = "reward";
+            if (what) {
+                if (bad < 5) fprintf(stderr, "mismatch t=%d env=%lld: %s\n", t, i, what);
                 bad++;
             }
         }
     printf("parity: %lld mismatching rows of %lld\n", bad, (long long)T * W);
+    /* stream position of every checked env's current game: ctl position minus its queued deals' draws (header-only
+     * decode) against the oracle's draws, which never draws ahead */
+    long long badpos = 0, queued = 0;
+    if (info.state_words != info.game_words + (info.deal_queue_depth ? 1 + 2 * info.deal_queue_depth : 0)) {
+        fprintf(stderr, "state_words %d != game_words %d + queue of %d\n", info.state_words, info.game_words,
+                info.deal_queue_depth);
+        return 7;
+    }
+    uint32_t* words = (uint32_t*)malloc(sizeof(uint32_t) * info.state_words);
+    for (long long i = 0; i < W; i++) {
+        uint32_t ctl;
+        CHECK(cs_get_env_state(h, i, words, info.state_words));
+        CHECK(cs_get_rng_ctl(h, i, &ctl));
+        const uint32_t q = queued_draws(words, &info);
+        queued += q != 0;
+        const uint32_t pos = ((ctl & (game == CS_GAME_DOUDIZHU ? 0x7FFu : 0x3FFFu)) + (uint32_t)info.rng_period - q) %
+                             (uint32_t)info.rng_period;
+        if (pos != (uint32_t)(or_batch_draws(b, i) % (uint64_t)info.rng_period)) {
+            if (badpos < 5) fprintf(stderr, "stream position env=%lld: %u vs oracle %llu\n", i, pos,
+                                    (unsigned long long)(or_batch_draws(b, i) % (uint64_t)info.rng_period));
+            badpos++;
+        }
+    }
+    printf("deal queue depth %d: %lld of %lld envs hold queued deals; stream positions: %lld mismatching\n",
+           info.deal_queue_depth, queued, W, badpos);
+    bad += badpos;
     cs_destroy(h);
     return bad ? 6 : 0;
 }
