@@ -71,7 +71,12 @@ typedef struct {
  *                                  no-limit: 52 card bits, then my chips and the largest chips in the pot)
  *   legal  uint8  [n][legal_bytes] legal-action bitmask, bit a of byte a/8 (LSB first) = action id a
  *   player uint8  [n]              current player id (Env.get_player_id)
- *   reward float  [n][num_players] payoffs of the transition (non-zero only where done; Env.get_payoffs)
+ *   reward float  [n][num_players] payoffs of the transition (non-zero only where done; Env.get_payoffs). f32 of the
+ *                                  reference's float64 payoffs, and exact for every payoff a game can reach: Leduc
+ *                                  (judger.py:50-56) splits total / #winners among at most 2 winners (2 cards per
+ *                                  rank; 3..5 players included), so its payoffs are multiples of 0.25; hold'em pays
+ *                                  whole chips (/ 2 big blinds in Limit), Blackjack +-1 / 0, DouDizhu 0 / 1
+ *                                  (tests/test_reward_precision.py enumerates them)
  *   done   uint8  [n]              1 if the game is over after this call (Env.is_over)
  * Any pointer may be NULL to skip that output. */
 typedef struct {

@@ -663,6 +663,18 @@ __device__ __forceinline__ void row_write_sparse(uint32_t* lds, const uint32_t (
     }
 }
 
+// XCD-aware block order: the dispatcher hands block b to XCD b % 8 (MI355X: 8 XCDs, each with its own L2), so with
+// the identity map neighbouring env ranges -- whose trajectory rows share 128-B lines where a row is not a line
+// multiple (DouDizhu's 901 / 3 434-byte rows) -- are written through different L2s, and every shared line reaches HBM
+// as two partial writes. xcd_block maps block b to env-block x * q + min(x, r) + b / 8 (x = b % 8, nb = 8 q + r): each
+// XCD takes one contiguous eighth of the env range. A bijection of [0, nb) for any nb (results do not depend on it).
+constexpr int NUM_XCD = 8;
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb)
+{
+    const uint32_t x = b % NUM_XCD, q = nb / NUM_XCD, r = nb % NUM_XCD;
+    return x * q + (x < r ? x : r) + b / NUM_XCD;
+}
+
 // set bit p of a multi-word bitmap without dynamic register indexing
 template <int NB>
 __device__ __forceinline__ void set_bit(uint32_t (&bits)[NB], int p)

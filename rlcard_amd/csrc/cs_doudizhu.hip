@@ -40,7 +40,7 @@ constexpr int MASK_WORDS = MASK_PAD + KTH_LANES * KTH_WORDS + MASK_PAD;
 constexpr int NSEG = 20;                          // 54-bit obs blocks (16 used) + zero tail
 constexpr int BV_WORDS = 32;                      // obs bits (912 + 16 front pad) as dwords
 #ifndef CS_PROF_DDZ
-#define CS_PROF_DDZ 0   // profiling only (wrong outputs): 1 skip legal rows, 2 skip obs rows, 4 skip build_obs (one-env
+#define CS_PROF_DDZ 0   // profiling only (wrong outputs): 32 no table loads in the legal build, 1 skip legal rows, 2 skip obs rows, 4 skip build_obs (one-env
                         // kernels), 16 skip build_obs2 (pair kernel)
 #endif
 
@@ -389,7 +389,8 @@ __device__ __forceinline__ void test_listed(uint32_t t0, uint32_t nl, uint64_t h
         dw[q] = ent[q] ? L.lst[e & (LIST_RING - 1)] : 0u;
         id[q] = dw[q] * 32u + (uint32_t)(lane & 31);
         live[q] = ent[q] && id[q] < (uint32_t)PASS;
-        cnt[q] = live[q] ? tb.cnt[id[q]] : ~0ull;
+        if constexpr ((CS_PROF_DDZ & 32) != 0) cnt[q] = live[q] ? simple_cnt(id[q], (uint32_t)tb.bomb_lo) : ~0ull;   // profiling
+        else cnt[q] = live[q] ? tb.cnt[id[q]] : ~0ull;
     }
 #pragma unroll
     for (int q = 0; q < PAIRS; q++) {
@@ -858,6 +859,16 @@ constexpr int NCH = (ND + HW - 1) / HW;              // 27 chunks of 32 mask dwo
 #ifndef CS_DDZ_SIMPLE
 #define CS_DDZ_SIMPLE 1   // bit 0: the fast path's candidates, bit 1: the chosen action's entries from simple_cnt / _gid (bit 1 measured 11 % slower: the select puts the table load's wait before the row stores)
 #endif
+#ifndef CS_DDZ_XCD
+#define CS_DDZ_XCD 1   // k_rollout2 blocks in XCD-aware order (cs_device.h xcd_block): rows shared by neighbouring blocks
+                       // meet in one L2
+#endif
+#ifndef CS_DDZ_ROWSTRIDE_L   // profiling builds only (tools/place_probe3.py PP_PAD): rows written at a padded stride
+#define CS_DDZ_ROWSTRIDE_L LB
+#endif
+#ifndef CS_DDZ_ROWSTRIDE_O
+#define CS_DDZ_ROWSTRIDE_O OBS
+#endif
 #ifndef CS_DDZ_CLEAN
 #define CS_DDZ_CLEAN 1   // zero only the dwords a step wrote, after its row is out (full zeroing when the list wrapped)
 #endif
@@ -927,7 +938,8 @@ __device__ __forceinline__ void test_listed2(uint32_t t0, uint32_t lim, uint64_t
         dw[q] = ent[q] ? L.lst[e & (LIST_RING - 1)] : 0u;
         id[q] = dw[q] * 32u + (uint32_t)hl;
         live[q] = ent[q] && id[q] < (uint32_t)PASS;
-        cnt[q] = live[q] ? tb.cnt[id[q]] : ~0ull;
+        if constexpr ((CS_PROF_DDZ & 32) != 0) cnt[q] = live[q] ? simple_cnt(id[q], (uint32_t)tb.bomb_lo) : ~0ull;   // profiling
+        else cnt[q] = live[q] ? tb.cnt[id[q]] : ~0ull;
     }
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -978,7 +990,9 @@ __device__ __forceinline__ void fast_finish(const Fast& f, uint64_t h, const Tab
     uint64_t cnt = f.cnt;
     // table loads only where a candidate is not simple (~5 % of these steps), waited for inside this branch: on gfx950
     // a load's wait also waits for every earlier store (vmcnt counts both), here the previous step's row stores
-    if (__ballot(f.load)) cnt = f.load ? tb.cnt[f.id] : cnt;
+    if constexpr ((CS_PROF_DDZ & 32) == 0) {   // profiling builds only: bit 5 drops the table loads of the legal build
+        if (__ballot(f.load)) cnt = f.load ? tb.cnt[f.id] : cnt;
+    }
     const bool pass = f.cand && contains(h, cnt);
     const uint32_t m = half32(__ballot(pass), lane);
     const uint32_t dw = f.id >> 5;
@@ -1279,7 +1293,8 @@ __global__ __launch_bounds__(PBLOCK, CS_DDZ_PAIR_MINW) void k_rollout2(PairArgs 
     load_tab(tl, tb);                 // every thread of the block, before any wave leaves
     const int lane = (int)(threadIdx.x & (WAVE - 1)), hl = lane & (HW - 1), hf = lane >> 5;
     const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
-    const int64_t env = (int64_t)blockIdx.x * (2 * PWPB) + 2 * wid + hf;
+    const uint32_t bx = CS_DDZ_XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int64_t env = (int64_t)bx * (2 * PWPB) + 2 * wid + hf;
     const bool valid = env < n;
     if (!__ballot(valid)) return;
     PairLds (&PL)[2] = lds[wid];
@@ -1355,7 +1370,7 @@ __global__ __launch_bounds__(PBLOCK, CS_DDZ_PAIR_MINW) void k_rollout2(PairArgs 
             }
         }
         wave_sync_lds();
-        const uint32_t lmis = (uint32_t)(((uintptr_t)out.legal + (uint64_t)row * LB) & 15u);   // the image's shift
+        const uint32_t lmis = (uint32_t)(((uintptr_t)out.legal + (uint64_t)row * CS_DDZ_ROWSTRIDE_L) & 15u);   // the image's shift
         const Cand cd = cand_of(e, tb, tl);
         const Fast fst = fast_issue(e, cd, tb, L, lane, valid && (kfl & 1) == 0);   // kernel flag bit 0: A/B only
         Legal lg = build_legal2(e, cd, tb, tl, L, lmis, lane, valid && !fst.fast);
@@ -1373,8 +1388,8 @@ __global__ __launch_bounds__(PBLOCK, CS_DDZ_PAIR_MINW) void k_rollout2(PairArgs 
         const uint32_t ga = play ? (sa ? simple_gid(a, (uint32_t)tb.bomb_lo, (uint32_t)tb.bomb_g) : (uint32_t)tb.gid[a]) : 0u;
         if (valid && !cd.leading && hl == 0) ((uint8_t*)L.mask)[16u + lmis + PASS / 8] |= (uint8_t)(1u << (PASS & 7));
         wave_sync_lds();
-        write_rows2(L, valid && !(CS_PROF_DDZ & 2) ? (uint8_t*)out.obs + row * OBS : nullptr,
-                    valid && !(CS_PROF_DDZ & 1) ? (uint8_t*)out.legal + row * LB : nullptr, lane);
+        write_rows2(L, valid && !(CS_PROF_DDZ & 2) ? (uint8_t*)out.obs + row * CS_DDZ_ROWSTRIDE_O : nullptr,
+                    valid && !(CS_PROF_DDZ & 1) ? (uint8_t*)out.legal + row * CS_DDZ_ROWSTRIDE_L : nullptr, lane);
         if constexpr (CS_DDZ_CLEAN != 0) {
             // clean after the row is out: zero the dwords this step wrote (all listed unless the list ring wrapped)
             // and the pass byte, instead of the whole image at the next step

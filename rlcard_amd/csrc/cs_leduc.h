@@ -59,6 +59,7 @@ struct Leduc {
     static constexpr int MIN_WAVES = CS_LEDUC_MIN_WAVES;  // rollout waves per SIMD the register budget must allow
     static constexpr int EPW = 64;        // rollout envs per wave (lane_ctx)
     static constexpr bool STORES_LAST = true;   // k_rollout: the step's rows after its restage loads (cs_skeleton.h)
+    static constexpr bool REWARD_PAIRS = true;  // k_rollout: reward rows as 16-B stores of two envs (cs_skeleton.h)
     static constexpr int REFILL_K = CS_LEDUC_REFILL_K;    // 1: refills are rare here, and K = 2 costs 12 VGPRs = 1 wave/SIMD
     __device__ __forceinline__ void bind(uint32_t*, const GameParams&) {}
     enum { CALL = 0, RAISE = 1, FOLD = 2, CHECK = 3 };

@@ -54,13 +54,14 @@ struct LaneCtx {
 
 // EPW envs per wave (lanes >= EPW idle): 64 everywhere but the rollouts of games with too few envs to fill the chip
 // (Limit's 262 144 envs are 4 waves per SIMD at 64 per wave; half-full waves double that -- the step is latency-bound)
-template <int EPW = WAVE>
+template <int EPW = WAVE, bool XCD = false>
 __device__ __forceinline__ LaneCtx lane_ctx(int64_t n)
 {
     LaneCtx c;
     c.lane = threadIdx.x & (WAVE - 1);
     c.wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // wave-uniform: wave_first lives in SGPRs
-    c.wave_first = ((int64_t)blockIdx.x * WAVES_PER_BLOCK + c.wid) * EPW;
+    const int64_t bx = XCD ? (int64_t)xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;   // cs_device.h
+    c.wave_first = (bx * WAVES_PER_BLOCK + c.wid) * EPW;
     c.env = c.wave_first + c.lane;
     const int64_t left = n - c.wave_first;
     c.nvalid = left >= EPW ? EPW : (left > 0 ? (int)left : 0);
@@ -149,6 +150,9 @@ struct SparseK<G, std::void_t<decltype(G::SPARSE_K)>> {
 #ifndef CS_STORES_LAST
 #define CS_STORES_LAST -1
 #endif
+#ifndef CS_ROLLOUT_XCD
+#define CS_ROLLOUT_XCD 0   // k_rollout blocks in XCD-aware order (cs_device.h xcd_block); A/B knob
+#endif
 template <class G, class = void>
 struct StoresLast {
     static constexpr bool value = CS_STORES_LAST == 1;
@@ -182,16 +186,27 @@ __device__ __forceinline__ void emit_reward(float* reward, int64_t row, const fl
 }
 
 // Two-player reward rows (8 B) of the rollout as 16-B stores: even lanes take their odd neighbour's pair (one DPP
-// row shift) and store both rows at once. All lanes call (invalid lanes hold zeros). CS_REWARD_PAIRS=0: one 8-B store
-// per lane. Measured: the 8-B nontemporal reward rows cost ~1.8x their bytes in WRITE_SIZE (Leduc 1.6 GB
-// per launch); pairs bring WRITE_SIZE to the algorithmic bytes but ran slower (4.59 -> 4.78 ms Leduc, 2.67 -> 2.80
-// Limit, same box): off.
+// row shift) and store both rows at once. All lanes call (invalid lanes hold zeros). Per game (G::REWARD_PAIRS,
+// default off; CS_REWARD_PAIRS = 0 / 1 / 2 overrides every two-player game for A/B builds); off: one 8-B store per
+// lane. Measured: the 8-B nontemporal reward rows cost ~1.8x their bytes in WRITE_SIZE (Leduc 1.6 GB per
+// launch); pairs bring WRITE_SIZE to the algorithmic bytes. With the rows stored where they were produced they ran
+// slower (4.59 -> 4.78 ms Leduc, 2.67 -> 2.80 Limit, round 2); with Leduc's rows after the step's loads (round 5,
+// StoresLast) 3.95 -> 3.86 ms: on for Leduc.
 #ifndef CS_REWARD_PAIRS
-#define CS_REWARD_PAIRS 0
+#define CS_REWARD_PAIRS -1
 #endif
+template <class G, class = void>
+struct RewardPairsOf {
+    static constexpr int value = 0;
+};
+template <class G>
+struct RewardPairsOf<G, std::void_t<decltype(G::REWARD_PAIRS)>> {
+    static constexpr int value = G::REWARD_PAIRS ? 1 : 0;
+};
 template <class G>
 struct RewardPairs {
-    static constexpr bool value = CS_REWARD_PAIRS && G::P == 2;
+    static constexpr int mode = CS_REWARD_PAIRS >= 0 ? CS_REWARD_PAIRS : RewardPairsOf<G>::value;
+    static constexpr bool value = mode != 0 && G::P == 2;
 };
 // CS_REWARD_PAIRS=2: the wave's 2 x EPW reward dwords transposed so that lane l stores dword l (and 64 + l): fully
 // coalesced 4-B stores (4 ds_bpermute per step)
@@ -605,7 +620,7 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
     uint8_t* const sbuf = args.sbuf;
     CS_SMEM_ROWS(G, G::EPW);
     __shared__ __attribute__((aligned(16))) uint8_t stage[WAVES_PER_BLOCK][StageBytes<G>::value];
-    const LaneCtx c = lane_ctx<G::EPW>(n);
+    const LaneCtx c = lane_ctx<G::EPW, CS_ROLLOUT_XCD != 0>(n);
     RingLane<G::STAGE_MODE> m = ring_lane<G::STAGE_MODE>(mt, ctl, c);
     constexpr bool SL = StoresLast<G>::value;
     // MT staging needs both blocks valid at every restage, i.e. the cooperative refill (flag bit 0 off);
@@ -782,7 +797,7 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
         auto store_reward_pairs = [&]() {
 #ifndef CS_PROF_NO_SMALL
             if constexpr (RewardPairs<G>::value) {
-                if constexpr (CS_REWARD_PAIRS == 2) emit_reward_t<G::EPW>(reward, rowbase, r, c);
+                if constexpr (RewardPairs<G>::mode == 2) emit_reward_t<G::EPW>(reward, rowbase, r, c);
                 else emit_reward_pairs(reward, rowbase, r, c);
             }
 #endif

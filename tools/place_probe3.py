@@ -50,8 +50,15 @@ def main():
     v = VecEnv(game, n, seed=42, device=0)
     v.reset()
     keep = []
-    trajs = [('torch%d' % i, v.new_traj_out(T)) for i in range(K)]
-    trajs += [('contig%d' % i, contiguous_traj(v, T, hip, keep)) for i in range(Cn)]
+    pad = [int(x) for x in os.environ.get('PP_PAD', '').split(',') if x]   # legal, obs row strides of a padded build
+
+    def padded(tr):
+        if pad:
+            tr['legal'] = torch.empty((T, n, pad[0]), dtype=torch.uint8, device=0)
+            tr['obs'] = torch.empty((T, n, pad[1]), dtype=torch.uint8, device=0)
+        return tr
+    trajs = [('torch%d' % i, padded(v.new_traj_out(T))) for i in range(K)]
+    trajs += [('contig%d' % i, contiguous_traj(v, T, hip, keep)) for i in range(Cn if not pad else 0)]
     t = 0
     for _ in range(bench.precondition_launches(game, T, v)):
         v.rollout(T, 5, t, out=trajs[0][1])

@@ -14,6 +14,7 @@
 //                      R = 1: wavemajor, R = 4: blockmajor)
 //   mode 9 packed_nt0  mode 1 with default-policy stores
 //   mode 12 planes     rec [T][3][ts][16]: the 48-B record as three 16-B planes (each wave store 1 KB contiguous)
+//   mode 13 ddz        DouDizhu's two row tensors (legal 3 434 B at off_legal, obs 901 B), 2 envs per wave; 14: nt
 //   mode 11 chunks     one sweep of the buffer, wave w writes R consecutive 1-KB pieces (a block: 4 R KB); T = 1
 // ts = rows per step (n + pad). Built by hand: hipcc -O3 -shared -fPIC --offload-arch=gfx950 -o tools/libwpat.so tools/wpat.hip
 #include <hip/hip_runtime.h>
@@ -72,6 +73,16 @@ __global__ __launch_bounds__(256) void k_wpat(WArgs a)
                 st<NT>((uint64_t*)(a.base + a.off_reward) + row, (uint64_t)x * 3u);
                 st<NT>(a.base + a.off_done + row, (uint8_t)(x >> 24));
             }
+        } else if constexpr (MODE == 13 || MODE == 14) {   // DouDizhu rows: 2 envs per wave, 3 434 + 901 B each
+            // (13: default-policy stores, 14: nontemporal); spans rounded out to 16-B chunks (neighbours overlap)
+            constexpr bool NT = MODE == 14;
+            const int64_t e0 = (int64_t)t * a.ts + 2 * wave;
+            const int64_t lb = e0 * 3434, ob = e0 * 901;
+            uint8_t* lrow = a.base + a.off_legal + (lb & ~15ll);
+            uint8_t* orow = a.base + (ob & ~15ll);
+            const int lq = (int)(((lb & 15) + 6868 + 15) >> 4), oq = (int)(((ob & 15) + 1802 + 15) >> 4);
+            for (int q = lane; q < lq; q += 64) st<NT>((u32x4*)lrow + q, v);
+            for (int q = lane; q < oq; q += 64) st<NT>((u32x4*)orow + q, v);
         } else if constexpr (MODE == 12) {   // planes: rec [T][3][ts][16], each store one 1-KB piece of a plane
 #pragma unroll
             for (int j = 0; j < 3; j++) st<true>((u32x4*)(a.base + (((int64_t)t * 3 + j) * a.ts + env) * 16), v);
@@ -115,6 +126,8 @@ extern "C" int wpat_run(const WArgs* a, int lds_bytes, void* stream)
     case 7: hipLaunchKernelGGL(k_wpat<7>, grid, dim3(256), lds_bytes, s, *a); break;
     case 8: hipLaunchKernelGGL(k_wpat<8>, grid, dim3(256), lds_bytes, s, *a); break;
     case 9: hipLaunchKernelGGL(k_wpat<9>, grid, dim3(256), lds_bytes, s, *a); break;
+    case 13: hipLaunchKernelGGL(k_wpat<13>, grid, dim3(256), lds_bytes, s, *a); break;
+    case 14: hipLaunchKernelGGL(k_wpat<14>, grid, dim3(256), lds_bytes, s, *a); break;
     case 12: hipLaunchKernelGGL(k_wpat<12>, grid, dim3(256), lds_bytes, s, *a); break;
     case 11: hipLaunchKernelGGL(k_wpat<11>, grid, dim3(256), lds_bytes, s, *a); break;
     default: return -1;

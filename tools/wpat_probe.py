@@ -17,7 +17,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 NAMES = {0: 'split', 1: 'packed', 2: 'wavemajor', 3: 'packedlane', 4: 'blockmajor', 5: 'obsonly', 6: 'split_nt0',
-         7: 'work', 8: 'grouped', 9: 'packed_nt0', 10: 'torchfill', 11: 'chunks', 12: 'planes'}
+         7: 'work', 8: 'grouped', 9: 'packed_nt0', 10: 'torchfill', 11: 'chunks', 12: 'planes', 13: 'ddz', 14: 'ddz_nt'}
 
 
 class _Dev:
@@ -66,6 +66,9 @@ def main():
     al = lambda s: (s + (2 << 20) - 1) // (2 << 20) * (2 << 20)
     size = max(al(t_ * (n_ + max(pads)) * 36) + 4 * al(t_ * (n_ + max(pads))) + al(t_ * (n_ + max(pads)) * 8)
                for n_, t_ in shapes) + (2 << 20)
+    if 13 in modes or 14 in modes:
+        size = max(size, max(al(t_ * (n_ + max(pads)) * 901) + al(t_ * (n_ + max(pads)) * 3434) + (8 << 20)
+                             for n_, t_ in shapes))
     bufs, raws = [], []
     for i in range(a.torch):
         t = torch.empty(size, dtype=torch.uint8, device=0)
@@ -88,6 +91,13 @@ def main():
             views[ptr][:T * n * 12].fill_(float(work))
             return
         ts = n + pad
+        if mode in (13, 14):   # DouDizhu rows: n envs = 2 per wave (grid n / 2 envs' lanes), legal after the obs rows
+            ts = n + pad   # rows per step: a padded step stride (pad rows), the env count stays n
+            w = WArgs(ptr, al(T * ts * 901) + (2 << 20), 0, 0, 0, 0, 32 * n, ts, T, work, mode, R, dm, xcd)   # n / 2 waves
+            assert w.off_legal + T * ts * 3434 + 4096 <= size, 'ddz rows exceed the buffer'
+            rc = lib.wpat_run(C.byref(w), lds, C.c_void_p(stream.cuda_stream))
+            assert rc == 0, rc
+            return
         if mode == 11:   # the same bytes as one sweep of R-KB wave pieces
             assert (T * n * 48) % (R * 1024 * 2048) == 0, 'chunk size must tile the sweep'
             n, T, ts = T * n * 48 // (R * 1024) * 64, 1, 0
@@ -106,7 +116,7 @@ def main():
     dms = [int(x) for x in a.data.split(',')]
     xcds = [int(x) for x in a.xcd.split(',')]
     cfgs = [(m, w, p, l, r, si, dm, xcd) for si in range(len(shapes)) for l in ldss for w in works for m in modes
-            for p in (pads if m in (0, 1, 3, 5, 6, 12) else [0]) for r in (groups if m in (8, 11) else [0])
+            for p in (pads if m in (0, 1, 3, 5, 6, 12, 13, 14) else [0]) for r in (groups if m in (8, 11) else [0])
             for dm in (dms if m != 10 else [0]) for xcd in (xcds if m != 10 else [0])]
     lab = lambda c: '%s/w%d/p%d/l%d%s%s%s' % (NAMES[c[0]][:8], c[1], c[2], c[3] // 1000,
                                              '/R%d' % c[4] if c[0] in (8, 11) else '', '/s%d' % c[5] if c[5] else '',
