@@ -205,6 +205,10 @@ def main():
                     help='skip the CS_RNG_PHILOX phase (reported under "rng_philox")')
     ap.add_argument('--no-precondition', dest='precondition', action='store_false',
                     help='time from freshly seeded streams (optimistic: no MT block refills yet)')
+    ap.add_argument('--select', type=int, default=3,
+                    help='trajectory placement selection: allocate this many candidate trajectories, time the '
+                         'placement probe (cs_traj_probe) on each and run on the fastest (1: off); reported under '
+                         '"placement"')
     ap.add_argument('--placement', type=int, default=3,
                     help='N=1: time a few launches into this many fresh trajectory allocations after the timed region '
                          '(untimed context under "placement"; 0: off)')
@@ -256,7 +260,8 @@ def main():
     N = args.envs or GAMES[game]['envs']
     env = ShardedVecEnv(game, N, rank, seed=42, device=local)   # global envs [rank*N, (rank+1)*N)
     env.reset()
-    traj = env.new_traj_out(T)
+    traj = env.new_traj_out(T, select=args.select)
+    probe_ms = list(getattr(env, 'placement_probe_ms', None) or [])
 
     stream = torch.cuda.current_stream()
     t_launch = 0
@@ -323,8 +328,10 @@ def main():
         # allocations -- the kernel time follows where the output buffers land in HBM, so a single allocation's
         # time is one draw from this spread
         per = [kernel_ms]
+        other_probe = []
         for _ in range(args.placement):
             other = env.new_traj_out(T)
+            other_probe.append(env.probe_traj(other, T))
             ms = []
             for k in range(4):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -336,10 +343,10 @@ def main():
                 ms.append(e0.elapsed_time(e1))
             per.append(sorted(ms)[len(ms) // 2] if len(ms) % 2 else sum(sorted(ms)[1:3]) / 2)
             del other
-        placement = dict(kernel_ms_per_allocation=per,
+        placement = dict(kernel_ms_per_allocation=per, probe_ms_per_allocation=[None] + other_probe,
                          note='untimed: kernel ms per launch of the timed allocation (first) and of %d fresh '
-                              'trajectory allocations (median of 4 launches each); not part of value'
-                              % args.placement)
+                              'trajectory allocations without selection (median of 4 launches each; their placement '
+                              'probe ms beside); not part of value' % args.placement)
         torch.cuda.empty_cache()
 
     gather_info = {}
@@ -437,8 +444,12 @@ def main():
                                   hip=state_snapshot.get('hip'), smi={k: smi.get(k) for k in keep},
                                   partition=(smi.get('partition') or {}).get('current_partition'),
                                   timed_window=power)
-        if placement is not None:
-            line['placement'] = placement
+        if placement is not None or probe_ms:
+            line['placement'] = dict(placement or {})
+            line['placement']['selection'] = dict(
+                candidates=len(probe_ms) or 1, probe_ms=probe_ms or None,
+                note='the timed trajectory is the fastest of the candidate allocations under the placement probe '
+                     '(cs_traj_probe: the rollout\'s writes, zeros, no game logic; DESIGN 7), chosen before warm-up')
         line.update(gather_info)
         if philox_info is not None:
             line['rng_philox'] = philox_info

@@ -151,6 +151,13 @@ int cs_observe(cs_handle* h, int32_t player, const cs_step_out* out, void* strea
 int cs_rollout(cs_handle* h, int32_t T, uint64_t policy_seed, uint64_t t0, uint64_t env_base, const cs_traj_out* out,
                void* stream);
 
+/* Placement probe of a trajectory allocation: zeros written into every non-NULL tensor of `out` ([T][n] rows, the
+ * cs_rollout layout) in the rollout's write order, without game logic or state change. Where a trajectory lands in HBM
+ * sets how fast it takes the rollout's writes (the same kernel runs 14 % slower in some allocations, and
+ * this probe's time separates them exactly), so a caller can time it on a few candidate allocations and keep the
+ * fastest (rlcard_amd.VecEnv.new_traj_out(select=k)). No reference counterpart (an allocation policy of this engine). */
+int cs_traj_probe(cs_handle* h, int32_t T, const cs_traj_out* out, void* stream);
+
 /* rlcard's reorganize (utils/utils.py:153-179: per player [state, action, reward, next_state, done]) and the DMC
  * return target (agents/dmc_agent/utils.py:97-163) of a cs_rollout trajectory of this handle, on the device. `traj`
  * needs player, reward and done. Games still running at the end of the window come out as next_t = -2. */

@@ -51,7 +51,7 @@ class DmcBatch(C.Structure):
 
 # every symbol include/cardsim.h declares (tests check the library exports all of them)
 SYMBOLS = ('cs_game_info_get', 'cs_create', 'cs_destroy', 'cs_seed', 'cs_reset', 'cs_step', 'cs_observe',
-           'cs_rollout', 'cs_transitions', 'cs_legal_lists', 'cs_action_features', 'cs_get_env_state',
+           'cs_rollout', 'cs_traj_probe', 'cs_transitions', 'cs_legal_lists', 'cs_action_features', 'cs_get_env_state',
            'cs_set_env_state', 'cs_copy_env_state', 'cs_set_step_record', 'cs_env_rng_words', 'cs_copy_env_rng',
            'cs_load_env_rng', 'cs_get_rng_ctl', 'cs_cfr_train', 'cs_debug_holdem_rank7', 'cs_debug_ddz_legal',
            'cs_debug_set_serial_refill', 'cs_debug_set_kernel_flags',
@@ -83,6 +83,7 @@ def lib():
     L.cs_step.argtypes = [vp, vp, C.POINTER(StepOut), vp]
     L.cs_observe.argtypes = [vp, i32, C.POINTER(StepOut), vp]
     L.cs_rollout.argtypes = [vp, i32, u64, u64, u64, C.POINTER(TrajOut), vp]
+    L.cs_traj_probe.argtypes = [vp, i32, C.POINTER(TrajOut), vp]
     L.cs_transitions.argtypes = [vp, i32, C.POINTER(TrajOut), C.POINTER(TransOut), vp]
     L.cs_legal_lists.argtypes = [vp, vp, i64, vp, vp, vp, vp]
     L.cs_action_features.argtypes = [vp, vp, i64, vp, vp]

@@ -371,6 +371,22 @@ int cs_dmc_select(const float* values, const int32_t* counts, const int64_t* off
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_dmc_select");
 }
 
+int cs_traj_probe(cs_handle* h, int32_t T, const cs_traj_out* out, void* stream)
+{
+    if (!h || !out) return fail(CS_E_INVALID, "null argument");
+    if (T <= 0) return fail(CS_E_INVALID, "T must be positive");
+    for (const void* p : {out->obs, out->legal, out->player, out->action, out->reward, out->done})
+        if (((uintptr_t)p & 15u) != 0) return fail(CS_E_INVALID, "trajectory tensors must be 16-byte aligned");
+    int r = set_device(h);
+    if (r != CS_OK) return r;
+    // envs per wave of the game's rollout kernel: DouDizhu two (k_rollout2), heads-up Limit / No-limit 32, else 64
+    const int32_t g = h->b.game, np = h->info.num_players;
+    const int32_t epw = g == CS_GAME_DOUDIZHU ? 2 : ((g == CS_GAME_LIMIT || g == CS_GAME_NOLIMIT) && np == 2 ? 32 : 64);
+    hipError_t e = cs::launch_traj_probe(h->b, T, *out, h->info.obs_dim, h->info.legal_bytes, h->info.action_bytes, epw,
+                                         (hipStream_t)stream);
+    return e == hipSuccess ? CS_OK : fail_hip(e, "cs_traj_probe");
+}
+
 int cs_transitions(cs_handle* h, int32_t T, const cs_traj_out* traj, const cs_trans_out* out, void* stream)
 {
     if (!h || !traj || !out) return fail(CS_E_INVALID, "null argument");

@@ -153,6 +153,8 @@ hipError_t launch_cfr(const Buffers& b, int32_t iterations, int64_t iteration0, 
                       hipStream_t s);
 
 // cs_traj.hip
+hipError_t launch_traj_probe(const Buffers& b, int32_t T, const cs_traj_out& tr, int32_t obs_dim, int32_t legal_bytes,
+                             int32_t action_bytes, int32_t epw, hipStream_t s);
 hipError_t launch_transitions(const Buffers& b, int32_t T, const cs_traj_out& tr, const cs_trans_out& o,
                               hipStream_t s);
 hipError_t launch_legal_lists(const Buffers& b, int32_t lb, const uint8_t* legal, int64_t rows, int32_t* counts,

@@ -171,6 +171,55 @@ __global__ __launch_bounds__(TBLOCK) void k_legal_wave(const uint8_t* __restrict
     }
 }
 
+// Trajectory placement probe (cs_traj_probe): zeros written into every output tensor of a T-step trajectory in the
+// rollout's order -- per step, each wave's span of EPW consecutive envs' rows of each tensor -- with no game logic.
+// Its time tells how fast this allocation takes the rollout's writes (the rollout's time follows it: DESIGN 7); the
+// host keeps the fastest of a few candidate allocations (VecEnv.new_traj_out(select=k)). 16-B nontemporal stores for
+// the span's whole chunks, single bytes for its ends: nothing outside a tensor is written.
+struct ProbeSpan {
+    uint8_t* base;
+    int32_t row;   // bytes per env row
+};
+__device__ __forceinline__ void probe_span(uint8_t* p, int64_t begin, int64_t end, int lane)
+{
+    const int64_t b16 = (begin + 15) & ~(int64_t)15, e16 = end & ~(int64_t)15;
+    if (b16 >= e16) {   // a span inside one chunk: bytes
+        for (int64_t k = begin + lane; k < end; k += WAVE) p[k] = 0;
+        return;
+    }
+    const u32x4_t z = {0u, 0u, 0u, 0u};
+    for (int64_t q = b16 + 16 * (int64_t)lane; q < e16; q += 16 * WAVE) __builtin_nontemporal_store(z, (u32x4_t*)(p + q));
+    if (lane < 16 && begin + lane < b16) p[begin + lane] = 0;
+    if (lane >= 16 && lane < 32 && e16 + (lane - 16) < end) p[e16 + (lane - 16)] = 0;
+}
+__global__ __launch_bounds__(TBLOCK) void k_traj_probe(ProbeSpan o0, ProbeSpan o1, ProbeSpan o2, ProbeSpan o3,
+                                                       ProbeSpan o4, ProbeSpan o5, int T, int64_t n, int epw)
+{
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t wave = (int64_t)blockIdx.x * (TBLOCK / WAVE) + __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+    const int64_t e0 = wave * epw;
+    if (e0 >= n) return;
+    const int64_t e1 = e0 + epw < n ? e0 + epw : n;
+    const ProbeSpan sp[6] = {o0, o1, o2, o3, o4, o5};
+    for (int t = 0; t < T; t++) {
+        const int64_t r0 = (int64_t)t * n;
+#pragma unroll
+        for (int k = 0; k < 6; k++)
+            if (sp[k].base) probe_span(sp[k].base, (r0 + e0) * sp[k].row, (r0 + e1) * sp[k].row, lane);
+    }
+}
+
+hipError_t launch_traj_probe(const Buffers& b, int32_t T, const cs_traj_out& tr, int32_t obs_dim, int32_t legal_bytes,
+                             int32_t action_bytes, int32_t epw, hipStream_t s)
+{
+    const ProbeSpan o0{(uint8_t*)tr.obs, obs_dim}, o1{(uint8_t*)tr.legal, legal_bytes}, o2{(uint8_t*)tr.player, 1},
+        o3{(uint8_t*)tr.action, action_bytes}, o4{(uint8_t*)tr.reward, 4 * b.num_players}, o5{(uint8_t*)tr.done, 1};
+    const int64_t waves = (b.n + epw - 1) / epw;
+    const dim3 grid((unsigned)((waves + TBLOCK / WAVE - 1) / (TBLOCK / WAVE)));
+    hipLaunchKernelGGL(k_traj_probe, grid, dim3(TBLOCK), 0, s, o0, o1, o2, o3, o4, o5, T, b.n, epw);
+    return hipGetLastError();
+}
+
 hipError_t launch_transitions(const Buffers& b, int32_t T, const cs_traj_out& tr, const cs_trans_out& o,
                               hipStream_t s)
 {

@@ -134,13 +134,38 @@ class VecEnv:
                        'cs_observe')
         return o
 
-    def new_traj_out(self, T, final_obs=False):
-        o = self.new_step_out((T,))
-        o['action'] = torch.empty((T, self.num_envs), dtype=self.action_dtype, device=self.device)
-        if final_obs:   # every player's observation where a game ended (Env.run's final states)
-            o['final_obs'] = torch.zeros((T, self.num_envs, self.num_players, self.obs_dim), dtype=torch.uint8,
-                                         device=self.device)
-        return o
+    def new_traj_out(self, T, final_obs=False, select=1):
+        """Trajectory buffers [T, N, ...] for rollout(). select = k > 1: allocate k candidates, time the placement
+        probe (probe_traj) on each and keep the fastest -- where a trajectory lands in HBM sets how fast it takes
+        the rollout's writes; the probe times of the candidates are left in self.placement_probe_ms."""
+        def one():
+            o = self.new_step_out((T,))
+            o['action'] = torch.empty((T, self.num_envs), dtype=self.action_dtype, device=self.device)
+            if final_obs:   # every player's observation where a game ended (Env.run's final states)
+                o['final_obs'] = torch.zeros((T, self.num_envs, self.num_players, self.obs_dim), dtype=torch.uint8,
+                                             device=self.device)
+            return o
+        if select <= 1:
+            return one()
+        cands = [one() for _ in range(int(select))]
+        times = [min(self.probe_traj(c, T) for _ in range(2)) for c in cands]
+        self.placement_probe_ms = times
+        best = min(range(len(cands)), key=lambda i: times[i])
+        return cands[best]
+
+    def probe_traj(self, traj, T=None):
+        """ms of one placement probe (include/cardsim.h cs_traj_probe: the rollout's writes, zeros, no state change)
+        over the trajectory `traj`, timed with events on the env's stream."""
+        T = int(T if T is not None else traj['player'].shape[0])
+        s = _abi.TrajOut(_ptr(traj['obs']), _ptr(traj['legal']), _ptr(traj['player']), _ptr(traj['action']),
+                         _ptr(traj['reward']), _ptr(traj['done']), None)
+        with torch.cuda.device(self.device):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            _abi.check(_abi.lib().cs_traj_probe(self._h, T, C.byref(s), self._stream()), 'cs_traj_probe')
+            e1.record()
+            e1.synchronize()
+        return e0.elapsed_time(e1)
 
     def rollout(self, T, policy_seed=0, t0=0, out=None, final_obs=False):
         """T lockstep steps of the uniform-random legal policy, auto-reset; -> trajectory dict of [T, N, ...]
