@@ -83,7 +83,8 @@ def lib():
     L.cs_step.argtypes = [vp, vp, C.POINTER(StepOut), vp]
     L.cs_observe.argtypes = [vp, i32, C.POINTER(StepOut), vp]
     L.cs_rollout.argtypes = [vp, i32, u64, u64, u64, C.POINTER(TrajOut), vp]
-    L.cs_traj_probe.argtypes = [vp, i32, C.POINTER(TrajOut), vp]
+    if hasattr(L, 'cs_traj_probe'):   # (older A/B builds lack it)
+        L.cs_traj_probe.argtypes = [vp, i32, C.POINTER(TrajOut), vp]
     L.cs_transitions.argtypes = [vp, i32, C.POINTER(TrajOut), C.POINTER(TransOut), vp]
     L.cs_legal_lists.argtypes = [vp, vp, i64, vp, vp, vp, vp]
     L.cs_action_features.argtypes = [vp, vp, i64, vp, vp]
