@@ -22,6 +22,7 @@
 #include "cs_ring.h"
 #include "cs_engine.h"
 #include "cs_leduc.h"
+#include "cs_dq.h"
 
 #pragma clang fp contract(off)
 
@@ -189,7 +190,8 @@ __global__ __launch_bounds__(256) void k_cfr_iteration(uint32_t* mt, uint32_t* c
     g.blank();
     if (valid) g.load(st, n, env);
     for (int p = 0; p < 2; p++) {
-        if (valid) g.reset(m);          // env.reset(): a new deal from the env's own stream
+        if (valid) game_reset_hbm(g, m, st, n, env);   // env.reset(): the next deal of the env's stream (its deal
+                                                        // queue first, cs_dq.h)
         ring_refill_wave(m, lane);      // all 64 lanes
         if (valid) traverse(g, p, iteration, t, recs, batched, ((int64_t)p * n + env) * REC_CAP);
     }

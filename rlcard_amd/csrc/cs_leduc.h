@@ -39,6 +39,9 @@
 #ifndef CS_LEDUC_STAGE_W
 #define CS_LEDUC_STAGE_W 64
 #endif
+#ifndef CS_LEDUC_DQ
+#define CS_LEDUC_DQ 0   // deals drawn ahead per env (cs_dq.h; 0 = none): a reset pops one, a lockstep pass refills
+#endif
 #ifndef CS_LEDUC_STAGE_R
 
 #define CS_LEDUC_STAGE_R 12
@@ -47,7 +50,11 @@
 namespace cs {
 
 struct Leduc {
-    static constexpr int OBS = 36, A = 4, P = 2, LB = 1, WORDS = 2, ACTION_BYTES = 1;
+    static_assert(CS_LEDUC_DQ == 0 || CS_LEDUC_DQ == 2 || CS_LEDUC_DQ == 4, "Leduc deal queue: 0, 2 or 4 deals");
+    static constexpr int GW = 2;   // game words; the deal queue (CS_LEDUC_DQ > 0) follows
+    static constexpr int DQ = CS_LEDUC_DQ;
+    static constexpr bool DQ_REGS = true, DQ_HBM = false;   // rollout: the queue words in registers
+    static constexpr int OBS = 36, A = 4, P = 2, LB = 1, WORDS = GW + (DQ > 0 ? 1 + 2 * DQ : 0), ACTION_BYTES = 1;
     static constexpr int NB = 2;  // obs bitmap words
     static constexpr bool RING = true;          // MT stream as the byte ring (cs_ring.h)
     static constexpr bool RAW_OBS = false;
@@ -128,8 +135,9 @@ struct Leduc {
     // each, and the stage positions are first-set searches: p0 (i=5), p1 (i=4, after p0), p2 = p1 + 1, p3 (i=2, after
     // p2), p4 = p3 + 1, p5 = p4 + 1 (the blind). false: the staged window does not hold the whole reset (the caller
     // runs the byte state machine instead).
+    // A deal as one word (the deal queue's entry, cs_dq.h): hand 0 | hand 1 << 3 | public << 6 | small blind << 9
     template <class Rng>
-    __device__ __forceinline__ bool reset_swar(Rng& rng)
+    __device__ __forceinline__ static bool deal_swar(Rng& rng, uint32_t& code)
     {
         const uint32_t k0 = rng.staged_offset();
         const uint32_t avail = k0 < rng.sn ? rng.sn - k0 : 0u, nv = avail < 16u ? avail : 16u;
@@ -166,33 +174,22 @@ struct Leduc {
         const uint32_t j1 = b[p0] & 7u, j2 = b[p1] & 7u, j3 = b[p2] & 3u, s = b[p5] & 1u;
         rng.advance_by(p5 + 1);
         // deck positions after the swaps (deck[i] = i before): 5 <- j1; 4 <- deck'[j2]; 3 <- deck''[j3]
-        h0 = (int)j1;
-        h1 = j2 == j1 ? 5 : (int)j2;
-        pub = j3 == j2 ? (j1 == 4 ? 5 : 4) : (j3 == j1 ? 5 : (int)j3);
-        deal_blinds((int)s);
+        const uint32_t hh0 = j1, hh1 = j2 == j1 ? 5u : j2;
+        const uint32_t pb = j3 == j2 ? (j1 == 4u ? 5u : 4u) : (j3 == j1 ? 5u : j3);
+        code = hh0 | hh1 << 3 | pb << 6 | s << 9;
         return true;
     }
 
-    __device__ __forceinline__ void deal_blinds(int s)
-    {
-        in0 = s == 0 ? 1 : 2;
-        in1 = s == 0 ? 2 : 1;
-        ptr = s;
-        r0 = in0; r1 = in1;
-        hr = 0; nrn = 0; rc = 0; f0 = 0; f1 = 0; over = 0;
-    }
-
     template <class Rng>
-    __device__ __forceinline__ void reset(Rng& rng)
+    __device__ __forceinline__ static uint32_t draw_deal(Rng& rng)
     {
 #ifdef CS_PROF_NO_RESET   // profiling builds only: wrong deals, timing of the reset
         rng.advance_by(7u);
-        h0 = 0; h1 = 2; pub = 4;
-        deal_blinds((int)(rng.pos & 1u));
-        return;
+        return 0u | 2u << 3 | 4u << 6 | (rng.pos & 1u) << 9;
 #endif
         if constexpr (Rng::kMode == STAGE_LDS && CS_LEDUC_RESET_SWAR) {
-            if (reset_swar(rng)) return;
+            uint32_t code;
+            if (deal_swar(rng, code)) return code;
         }
         uint32_t deck = 0x543210u;  // nibble i = card at deck position i
         uint32_t q = 0, s = 0;
@@ -225,8 +222,36 @@ struct Leduc {
             rng.advance_by(k - k0);
         }
         while (q < 6) take(rng.next8());
-        h0 = (deck >> 20) & 15; h1 = (deck >> 16) & 15; pub = (deck >> 12) & 15;
-        deal_blinds((int)s);
+        return ((deck >> 20) & 15u) | ((deck >> 16) & 15u) << 3 | ((deck >> 12) & 15u) << 6 | s << 9;
+    }
+
+    __device__ __forceinline__ void deal_blinds(int s)
+    {
+        in0 = s == 0 ? 1 : 2;
+        in1 = s == 0 ? 2 : 1;
+        ptr = s;
+        r0 = in0; r1 = in1;
+        hr = 0; nrn = 0; rc = 0; f0 = 0; f1 = 0; over = 0;
+    }
+
+    // Game.init_game from a deal word (draw_deal, or the deal queue's entry: cs_dq.h dq_reset)
+    __device__ __forceinline__ void reset_from(uint32_t e0, uint32_t)
+    {
+        h0 = (int)(e0 & 7u);
+        h1 = (int)((e0 >> 3) & 7u);
+        pub = (int)((e0 >> 6) & 7u);
+        deal_blinds((int)((e0 >> 9) & 1u));
+    }
+    template <class Rng>
+    __device__ __forceinline__ void make_deal(Rng& rng, uint32_t&, uint32_t& e0, uint32_t& e1) const
+    {
+        e0 = draw_deal(rng);
+        e1 = 0u;
+    }
+    template <class Rng>
+    __device__ __forceinline__ void reset(Rng& rng)
+    {
+        reset_from(draw_deal(rng), 0u);
     }
 
     template <class Rng>
