@@ -113,6 +113,8 @@ def lib():
     L.cs_version.restype = C.c_char_p
     for name in SYMBOLS:
         if name not in ('cs_destroy', 'cs_dmc_destroy', 'cs_last_error', 'cs_version'):
+            if name == 'cs_traj_probe' and not hasattr(L, name):   # older A/B builds (CARDSIM_LIB) lack it
+                continue
             getattr(L, name).restype = C.c_int
     _lib = L
     return L

@@ -65,8 +65,11 @@ struct Leduc {
     static constexpr int RESTAGE_B = CS_LEDUC_RESTAGE_B;  // lanes restaged per pass (loads in flight): 4 > 8 > 1
     static constexpr int MIN_WAVES = CS_LEDUC_MIN_WAVES;  // rollout waves per SIMD the register budget must allow
     static constexpr int EPW = 64;        // rollout envs per wave (lane_ctx)
-    static constexpr bool STORES_LAST = true;   // k_rollout: the step's rows after its restage loads (cs_skeleton.h)
-    static constexpr bool REWARD_PAIRS = true;  // k_rollout: reward rows as 16-B stores of two envs (cs_skeleton.h)
+    // k_rollout (cs_skeleton.h): rows stored where they are produced, 8-B reward rows. Stores-last + reward pairs
+    // (round 5) were 4.1 vs 5.1 ms on physically contiguous trajectories but 6-7 % slower on every torch allocation
+    // once the stores-first step compiled as well as round 4's (4.22 vs 4.51 ms, same box, same allocations)
+    static constexpr bool STORES_LAST = false;
+    static constexpr bool REWARD_PAIRS = false;
     static constexpr int REFILL_K = CS_LEDUC_REFILL_K;    // 1: refills are rare here, and K = 2 costs 12 VGPRs = 1 wave/SIMD
     __device__ __forceinline__ void bind(uint32_t*, const GameParams&) {}
     enum { CALL = 0, RAISE = 1, FOLD = 2, CHECK = 3 };

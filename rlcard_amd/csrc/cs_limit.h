@@ -427,6 +427,7 @@ struct Limit {
     static constexpr int MIN_WAVES = CS_LIMIT_MIN_WAVES;  // 4 waves/SIMD (LDS-bound with the 8-deal queue; at a 4-deal
                                                           // queue 5 beat 4 and 6, which spilled 40 VGPRs)
     static constexpr int EPW = CS_LIMIT_EPW;   // rollout envs per wave: 262 144 envs need half-full waves (lane_ctx)
+    static constexpr bool LANE_OPAQUE = false;   // k_rollout: lane id not made opaque per step (cs_skeleton.h LaneOpaque)
     static constexpr int REFILL_K = 2;   // stale blocks twisted per pass (see mt_refill_wave)
     __device__ __forceinline__ void bind(uint32_t*, const GameParams&) {}
     enum { CALL = 0, RAISE = 1, FOLD = 2, CHECK = 3 };

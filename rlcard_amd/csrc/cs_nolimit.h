@@ -71,6 +71,8 @@ struct Nolimit {
     static constexpr int RESTAGE_B = 8;
     static constexpr int MIN_WAVES = CS_NOLIMIT_MIN_WAVES;
     static constexpr int EPW = CS_NOLIMIT_EPW;
+    static constexpr bool LANE_OPAQUE = false;   // k_rollout: lane id not made opaque per step (cs_skeleton.h LaneOpaque)
+    static constexpr bool REWARD_OPAQUE = true;  // k_rollout: keeps the reward rows' nontemporal hint (RewardOpaque)
     static constexpr int REFILL_K = 2;
     enum { FOLD = 0, CHECK_CALL = 1, RAISE_HALF_POT = 2, RAISE_POT = 3, ALL_IN = 4 };
     enum { ALIVE = 0, FOLDED = 1, ALLIN = 2 };

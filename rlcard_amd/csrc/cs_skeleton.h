@@ -46,6 +46,23 @@ __device__ inline void mt_init_by_array(uint32_t* mt, const uint32_t* key, int k
     mt[0] = 0x80000000u;
 }
 
+#ifndef CS_WID_UNIFORM
+#define CS_WID_UNIFORM 1   // lane_ctx: the wave index through readfirstlane (A/B knob)
+#endif
+// k_rollout: the lane id made opaque at every step (per game, G::LANE_OPAQUE, default on; CS_LANE_OPAQUE = 0 / 1
+// overrides every game for A/B builds). Round 5, same box: Limit 8.18 -> 8.07 ms and No-limit 9.33 -> 9.10 without
+// it, Blackjack 20.62 -> 20.89 and Leduc even
+#ifndef CS_LANE_OPAQUE
+#define CS_LANE_OPAQUE -1
+#endif
+template <class G, class = void>
+struct LaneOpaque {
+    static constexpr bool value = CS_LANE_OPAQUE != 0;
+};
+template <class G>
+struct LaneOpaque<G, std::void_t<decltype(G::LANE_OPAQUE)>> {
+    static constexpr bool value = CS_LANE_OPAQUE >= 0 ? CS_LANE_OPAQUE == 1 : G::LANE_OPAQUE;
+};
 struct LaneCtx {
     int lane, wid;
     int64_t env, wave_first;
@@ -60,7 +77,7 @@ __device__ __forceinline__ LaneCtx lane_ctx(int64_t n)
 {
     LaneCtx c;
     c.lane = threadIdx.x & (WAVE - 1);
-    c.wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // wave-uniform: wave_first lives in SGPRs
+    c.wid = CS_WID_UNIFORM ? __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE) : (int)(threadIdx.x / WAVE);   // wave-uniform: wave_first lives in SGPRs
     const int64_t bx = XCD ? (int64_t)xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;   // cs_device.h
     c.wave_first = (bx * WAVES_PER_BLOCK + c.wid) * EPW;
     c.env = c.wave_first + c.lane;
@@ -173,11 +190,27 @@ __device__ __forceinline__ void emit_legal(uint8_t* legal, int64_t row, uint64_t
 #ifndef CS_REWARD_NT
 #define CS_REWARD_NT 1   // 0: default-policy 8-B reward stores (A/B knob)
 #endif
+// the 8-B reward row's value made opaque before its nontemporal store (per game, G::REWARD_OPAQUE, default off;
+// CS_REWARD_OPAQUE = 0 / 1 overrides every game): without it the optimizer may split the store back into two float
+// stores and drop the nontemporal hint on the way (No-limit's rollout); with it where the hint survives anyway
+// (Leduc, Limit) the step schedules worse (Leduc 4.23 -> 4.48 ms, round 5)
+#ifndef CS_REWARD_OPAQUE
+#define CS_REWARD_OPAQUE -1
+#endif
+template <class G, class = void>
+struct RewardOpaque {
+    static constexpr bool value = CS_REWARD_OPAQUE == 1;
+};
+template <class G>
+struct RewardOpaque<G, std::void_t<decltype(G::REWARD_OPAQUE)>> {
+    static constexpr bool value = CS_REWARD_OPAQUE >= 0 ? CS_REWARD_OPAQUE == 1 : G::REWARD_OPAQUE;
+};
 template <class G>
 __device__ __forceinline__ void emit_reward(float* reward, int64_t row, const float (&r)[G::P])
 {
     if constexpr (G::P == 2) {
-        const uint64_t v = (uint64_t)__float_as_uint(r[0]) | (uint64_t)__float_as_uint(r[1]) << 32;
+        uint64_t v = (uint64_t)__float_as_uint(r[0]) | (uint64_t)__float_as_uint(r[1]) << 32;
+        if constexpr (RewardOpaque<G>::value) asm volatile("" : "+v"(v));
         if constexpr (CS_REWARD_NT) out_store((uint64_t*)(reward + row * 2), v);
         else *(uint64_t*)(reward + row * 2) = v;
     } else {
@@ -593,13 +626,17 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
     refill<G>(m, c.lane, flags & 1);
     if (staged) restage<G>(m, stage[c.wid], c.lane, c.valid);
     PolicyRng pol;
+#ifndef CS_GENV_HOIST
+#define CS_GENV_HOIST 1   // the stores-first step: the policy counter's env id computed once, before the loop (A/B knob)
+#endif
+    [[maybe_unused]] const uint64_t genv0 = args.env_base + (uint64_t)c.env;
     for (int t = 0; t < T; t++) {
         const RolloutArgs& A = arg();
         // the lane id made opaque at every step, so lane-derived values (env id, row and LDS addresses) are recomputed
         // from it instead of held across the step -- at 6 waves per SIMD (80 VGPRs) the held copies were spilled, and
         // a spill reload waits on every store the wave has in flight (vmcnt)
         LaneCtx cl = c;
-        {
+        if constexpr (LaneOpaque<G>::value) {
             int ol = c.lane;
             asm volatile("" : "+v"(ol));
             cl.lane = ol;
@@ -618,6 +655,80 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
         const uint64_t lg = g.legal();
         uint32_t bits[G::NB];
         g.observe(p, bits);
+#ifndef CS_SF_PLAIN
+#define CS_SF_PLAIN 1   // A/B knob: the stores-first step written out in place (1) or through the lambdas below (0)
+#endif
+        if constexpr (!SL && CS_SF_PLAIN != 0) {
+            // each row stored where it is produced. Written out rather than through the stores-last path's lambdas:
+            // the same operations in that form compiled to a schedule 6 % slower for Leduc in every placement
+            // (round 5, same-box A/B against the round-4 build)
+            const uint64_t genv = CS_GENV_HOIST ? genv0 : A.env_base + (uint64_t)(c.wave_first + cl.lane);
+            const uint32_t pr = pol.at(seed, genv, t0 + (uint64_t)t, t == 0);
+            int a;
+            if constexpr (G::A <= 8) a = pick_legal_small<G::A>((uint32_t)lg, pr);
+            else a = G::A <= 32 ? pick_legal32((uint32_t)lg, pr) : pick_legal(lg, pr);
+#ifndef CS_PROF_NO_OBS
+            if constexpr (SparseObs<G>::value) {
+                uint32_t pos[SparseK<G>::value];
+                const uint32_t tail = g.observe_pos(p, pos);
+                row_write_sparse<G::OBS, G::EPW, SparseK<G>::value, G::RAW_OBS>(
+                    lds[c.wid], pos, obs + (rowbase + c.wave_first) * G::OBS, cl.lane, c.nvalid, !(flags & 4), tail);
+            } else {
+                emit_obs<G, G::EPW>(lds[c.wid], bits, obs, rowbase + c.wave_first, flags, cl);
+            }
+#endif
+            uint32_t zr = 0;   // see below (CS_ZERO_OPAQUE)
+            asm volatile("" : "+v"(zr));
+            float r[G::P];
+#pragma unroll
+            for (int k = 0; k < G::P; k++) r[k] = __uint_as_float(zr);
+            bool done = false;
+            if (c.valid) {
+                const int64_t row = rowbase + cl.env;
+#ifndef CS_PROF_NO_SMALL
+                emit_legal<G>(legal, row, lg);
+                out_store(player + row, (uint8_t)p);
+#endif
+                if constexpr (G::ACTION_BYTES == 1) out_store((uint8_t*)out.action + row, (uint8_t)a);
+                else out_store((int16_t*)out.action + row, (int16_t)a);
+                g.step(a, m);
+                done = g.is_over();
+                if (done) {
+                    game_payoffs(g, r, m);
+                    if (out.final_obs) {   // Env.run's final state of every player (envs/env.py:161-164)
+#pragma unroll
+                        for (int q = 0; q < G::P; q++) {
+                            uint32_t fb[G::NB];
+                            g.observe(q, fb);
+                            write_obs_direct<G>((uint8_t*)out.final_obs + (row * G::P + q) * G::OBS, fb);
+                        }
+                    }
+                }
+#ifndef CS_PROF_NO_SMALL
+                if constexpr (!RewardPairs<G>::value) emit_reward<G>(reward, row, r);
+                out_store(done_o + row, (uint8_t)done);
+#endif
+                if constexpr (DQ == 0) {
+                    if (done) g.reset(m);
+                }
+            }
+#ifndef CS_PROF_NO_SMALL
+            if constexpr (RewardPairs<G>::value) {
+                if constexpr (RewardPairs<G>::mode == 2) emit_reward_t<G::EPW>(reward, rowbase, r, c);
+                else emit_reward_pairs(reward, rowbase, r, c);
+            }
+#endif
+            if constexpr (DQ > 0) {   // (the lockstep refill of the queues: below)
+                constexpr uint32_t CM = (1u << DqOf<G>::cb) - 1u;
+                if (__ballot(c.valid && done && (q.get(0) & CM) == 0u)) {
+                    if (c.valid && (q.get(0) & CM) < (uint32_t)DQ) dq_push(g, m, q);
+                }
+                if (c.valid && done) dq_reset(g, m, q);
+            }
+            refill<G>(m, cl.lane, flags & 1);
+            if (staged) restage<G>(m, stage[c.wid], cl.lane, c.valid);
+            continue;
+        }
         // the policy counter's env id from scalars + the lane id at each step (a loop-invariant 64-bit value would be
         // one more pair of VGPRs held across the step -- spilled, and its reload waits on the step's stores)
         const uint64_t genv = A.env_base + (uint64_t)(c.wave_first + cl.lane);
