@@ -322,6 +322,15 @@ def main():
     if pw is not None:
         sampler.join(timeout=5)
 
+    # the timed allocation's write ceiling (untimed): the placement probe writes the rollout's trajectory bytes (zeros,
+    # the same tensors and order, no game logic), so its rate is what this allocation takes writes at
+    write_probe = None
+    if args.select > 0:
+        wp_ms = sorted(env.probe_traj(traj, T) for _ in range(3))[1]
+        wbytes = sum(traj[k].numel() * traj[k].element_size() for k in ('obs', 'legal', 'player', 'action', 'reward', 'done'))
+        write_probe = dict(ms=wp_ms, bytes=wbytes, gbs=wbytes / (wp_ms * 1e-3) / 1e9, kernel_over_probe=kernel_ms / wp_ms,
+                           note='untimed: cs_traj_probe on the timed trajectory after the timed region (median of 3): '
+                                'the trajectory bytes alone at this allocation\'s write rate')
     placement = None
     if world == 1 and args.placement > 0:
         # untimed context for `value` ("the 3.5 / 4.3 ms split"): the same launches into fresh trajectory
@@ -421,6 +430,8 @@ def main():
                          'alg_bytes_per_env_step': B, 'alg_bytes_per_launch': B * N * T,
                          'kernel_ms_per_launch': kernel_ms, 'kernel': 'k_rollout<%s>' % game},
         }
+        if write_probe is not None:
+            line['roofline']['write_probe'] = write_probe
         tr = measured_traffic(game, N, T, kernel_ms)
         if tr is not None:   # per launch, like `achieved`; from the profile of this exact configuration and kernels
             if tr['stale']:
