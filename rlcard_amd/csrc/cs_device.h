@@ -87,10 +87,23 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y)
     return y;
 }
 
+// the low byte of mt_temper(y) (bits 8.. differ): the last two steps only reach the low byte through bits 0..10 and
+// 18..25 of the second step's value y2, as y2 ^ (y2 >> 18) ^ ((y2 >> 3) & 0xF1) -- no left shift (a quarter-rate
+// instruction on gfx950) in the third step. Both maps are GF(2)-linear; equal on the 32 unit vectors.
+__device__ __forceinline__ uint32_t mt_temper_lo8(uint32_t y)
+{
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    return y ^ (y >> 18) ^ ((y >> 3) & 0xF1u);
+}
+
 __device__ __forceinline__ uint32_t mt_mix(uint32_t cur, uint32_t nxt, uint32_t far)
 {
-    uint32_t y = (cur & 0x80000000u) | (nxt & 0x7fffffffu);
-    return far ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+    // (cur & 0x80000000) | (nxt & 0x7fffffff) as one bitfield insert (v_bfi_b32) instead of and + and_or; y & 1 is
+    // nxt & 1, so the matrix term does not wait for the insert
+    uint32_t y;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(y) : "s"(0x7fffffffu), "v"(nxt), "v"(cur));
+    return far ^ (y >> 1) ^ ((0u - (nxt & 1u)) & 0x9908b0dfu);
 }
 
 // dst = twist(src), one lane, in-order (rare slow path and the seeding kernel)

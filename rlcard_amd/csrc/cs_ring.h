@@ -124,13 +124,19 @@ __device__ __forceinline__ void twist_regs(const uint32_t (&o)[10], uint32_t (&n
 #pragma unroll
     for (int c = 0; c < 10; c++) {
         uint32_t nxt;
-        if constexpr (CS_TWIST_DPP != 0)
-            nxt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)o[c], 0x130, 0xF, 0xF, false);   // wave_shl:1
-        else
+        if constexpr (CS_TWIST_DPP != 0) {
+            // wave_shl:1 without bound_ctrl: lane 63 has no source lane and keeps `old` -- the wrap word (the next
+            // chunk's lane 0) goes in as `old`, so the shift needs no select (chunk 9 wraps at lane 47: below)
+            const int old = c < 9 ? (int)__builtin_amdgcn_readlane(o[c < 9 ? c + 1 : 9], 0) : 0;
+            nxt = (uint32_t)__builtin_amdgcn_update_dpp(old, (int)o[c], 0x130, 0xF, 0xF, false);
+        } else {
             nxt = shfl(o[c], l1);
+        }
         if (c < 9) {
-            const uint32_t wrap = __builtin_amdgcn_readlane(o[c + 1], 0);
-            nxt = lane == 63 ? wrap : nxt;
+            if constexpr (CS_TWIST_DPP == 0) {
+                const uint32_t wrap = __builtin_amdgcn_readlane(o[c + 1], 0);
+                nxt = lane == 63 ? wrap : nxt;
+            }
         } else {
             const uint32_t n0 = __builtin_amdgcn_readlane(n[0], 0);
             nxt = lane == 47 ? n0 : nxt;
@@ -197,7 +203,7 @@ __device__ __forceinline__ void ring_gen_wave(gu32* wbuf, uint32_t lat, int lane
         for (int c = 0; c < 10; c++) {
             if constexpr (CS_RING_BYTE_ST) {
                 if (c < 9 || lane < 48)
-                    ((gu8*)(ring + slot * (MT_N / 4)))[64 * c + lane] = (uint8_t)mt_temper(n[c]);
+                    ((gu8*)(ring + slot * (MT_N / 4)))[64 * c + lane] = (uint8_t)mt_temper_lo8(n[c]);
             } else {
                 const int t = (int)(mt_temper(n[c]) & 255u);
                 const uint32_t t1 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x101, 0xF, 0xF, true);  // row_shl:1
