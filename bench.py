@@ -20,6 +20,7 @@ import hashlib
 import json
 import math
 import os
+import re
 import sys
 import time
 
@@ -75,15 +76,24 @@ def precondition_launches(game, T, vec):
     return int(math.ceil((vec.rng_first_refill + 2 * vec.rng_per_refill) / (g['draws_per_step'] * T)))
 
 
+def _code_only(text):
+    """C++ source without its comments and blank space (a comment edit does not change the kernels)"""
+    text = re.sub(r'/\*.*?\*/', ' ', text, flags=re.S)
+    text = re.sub(r'//[^\n]*', '', text)
+    return '\n'.join(' '.join(line.split()) for line in text.split('\n') if line.strip())
+
+
 def kernel_source_digest():
-    """sha256 (16 hex) of the engine's sources: a traffic profile is only reported for the kernels it measured."""
+    """sha256 (16 hex) of the engine's sources, comments stripped: a traffic profile is only reported for the kernels
+    it measured."""
     d = os.path.join(ROOT, 'rlcard_amd', 'csrc')
     h = hashlib.sha256()
     for f in sorted(os.listdir(d)):
         if f.endswith(('.hip', '.h', '.cpp', '.bin')) or f == 'Makefile':
             h.update(f.encode())
             with open(os.path.join(d, f), 'rb') as fh:
-                h.update(fh.read())
+                data = fh.read()
+            h.update(_code_only(data.decode()).encode() if f.endswith(('.hip', '.h', '.cpp')) else data)
     return h.hexdigest()[:16]
 
 

@@ -163,8 +163,9 @@ struct SparseK<G, std::void_t<decltype(G::SPARSE_K)>> {
 // for A/B builds): 1 = every trajectory store of the step after its refill / restage loads -- on gfx950 one counter
 // (vmcnt) tracks loads and stores in issue order, so a load issued after the rows waits until every row store is
 // acknowledged, a drain whose length is the HBM write latency of the moment, which depends on where the trajectory
-// landed in HBM (Leduc 4.05 -> 4.02 ms on torch allocations, 5.1 -> 4.1 on physically contiguous
-// ones); 0 = each row stored where it is produced (Limit: 8.1 vs 8.35 ms -- VALU-bound, the rows' live ranges cost more)
+// landed in HBM (Leduc 5.1 -> 4.1 ms on physically contiguous trajectories); 0 = each row stored
+// where it is produced: every game (Leduc 4.22 vs 4.51 ms on torch allocations once the stores-first step compiled as
+// well as round 4's; Limit 8.1 vs 8.35 -- VALU-bound, the rows' live ranges cost more)
 #ifndef CS_STORES_LAST
 #define CS_STORES_LAST -1
 #endif
@@ -225,7 +226,7 @@ __device__ __forceinline__ void emit_reward(float* reward, int64_t row, const fl
 // lane. Measured: the 8-B nontemporal reward rows cost ~1.8x their bytes in WRITE_SIZE (Leduc 1.6 GB per
 // launch); pairs bring WRITE_SIZE to the algorithmic bytes. With the rows stored where they were produced they ran
 // slower (4.59 -> 4.78 ms Leduc, 2.67 -> 2.80 Limit, round 2); with Leduc's rows after the step's loads (round 5,
-// StoresLast) 3.95 -> 3.86 ms: on for Leduc.
+// StoresLast) 3.95 -> 3.86 ms, but that form is off (see StoresLast): off everywhere.
 #ifndef CS_REWARD_PAIRS
 #define CS_REWARD_PAIRS -1
 #endif
