@@ -450,11 +450,7 @@ __device__ __forceinline__ void ring_restage_wave(RingLane<STAGE_LDS>& m, uint8_
                 uint32_t off = shfl(p4, s) + 4u * (uint32_t)col;
                 if (off >= RING) off -= RING;
                 const gu32* rp = (const gu32*)(uintptr_t)rb;
-#ifdef CS_PROF_NO_RESTAGE_LOAD   // profiling builds only: wrong bytes, timing without the restage's global loads
-                v[b] = off ^ (uint32_t)(uintptr_t)rp;
-#else
                 v[b] = ring_ld(rp + (off >> 2));
-#endif
             }
 #pragma unroll
             for (int b = 0; b < B; b++) *(uint32_t*)(area + src[b] * STRIDE + 4 * col) = v[b];
