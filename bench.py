@@ -219,6 +219,9 @@ def main():
                     help='trajectory placement selection: allocate this many candidate trajectories, time the '
                          'placement probe (cs_traj_probe) on each and run on the fastest (1: off); reported under '
                          '"placement"')
+    ap.add_argument('--select-by', choices=('rollout', 'probe'), default='rollout',
+                    help='how --select ranks its candidates: one untimed rollout launch per candidate after the '
+                         'preconditioning (default; exact), or the placement probe before it (no env steps)')
     ap.add_argument('--placement', type=int, default=3,
                     help='N=1: time a few launches into this many fresh trajectory allocations after the timed region '
                          '(untimed context under "placement"; 0: off)')
@@ -270,8 +273,10 @@ def main():
     N = args.envs or GAMES[game]['envs']
     env = ShardedVecEnv(game, N, rank, seed=42, device=local)   # global envs [rank*N, (rank+1)*N)
     env.reset()
-    traj = env.new_traj_out(T, select=args.select)
-    probe_ms = list(getattr(env, 'placement_probe_ms', None) or [])
+    by_rollout = args.select > 1 and args.select_by == 'rollout'
+    cands = [env.new_traj_out(T) for _ in range(args.select)] if by_rollout else None
+    traj = cands[0] if by_rollout else env.new_traj_out(T, select=args.select)
+    probe_ms = list(getattr(env, 'placement_probe_ms', None) or []) if not by_rollout else []
 
     stream = torch.cuda.current_stream()
     t_launch = 0
@@ -280,6 +285,25 @@ def main():
         env.rollout(T, policy_seed=5, t0=t_launch * T, out=traj)
         t_launch += 1
     torch.cuda.synchronize()
+    cand_ms = None
+    if by_rollout:
+        # placement selection by the kernel itself (untimed, in steady state): two launches into each candidate
+        # trajectory allocation, interleaved; the timed region runs on the fastest, the others are freed
+        cand_ms = [[] for _ in cands]
+        for r in range(2):
+            for i, c in enumerate(cands):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                env.rollout(T, policy_seed=5, t0=t_launch * T, out=c)
+                e1.record(stream)
+                t_launch += 1
+                torch.cuda.synchronize()
+                cand_ms[i].append(e0.elapsed_time(e1))
+        best = min(range(len(cands)), key=lambda i: min(cand_ms[i]))
+        traj = cands[best]
+        cand_ms = [min(x) for x in cand_ms]
+        cands = None
+        torch.cuda.empty_cache()
     w0 = time.perf_counter()
     for w in range(args.warmup):
         env.rollout(T, policy_seed=5, t0=t_launch * T, out=traj)
@@ -465,12 +489,19 @@ def main():
                                   hip=state_snapshot.get('hip'), smi={k: smi.get(k) for k in keep},
                                   partition=(smi.get('partition') or {}).get('current_partition'),
                                   timed_window=power)
-        if placement is not None or probe_ms:
+        if placement is not None or probe_ms or cand_ms:
             line['placement'] = dict(placement or {})
-            line['placement']['selection'] = dict(
-                candidates=len(probe_ms) or 1, probe_ms=probe_ms or None,
-                note='the timed trajectory is the fastest of the candidate allocations under the placement probe '
-                     '(cs_traj_probe: the rollout\'s writes, zeros, no game logic; DESIGN 7), chosen before warm-up')
+            if cand_ms:
+                line['placement']['selection'] = dict(
+                    candidates=len(cand_ms), by='rollout', rollout_ms=cand_ms,
+                    note='the timed trajectory is the fastest of the candidate allocations by one untimed rollout '
+                         'launch each (best of two, after the preconditioning; DESIGN 7)')
+            else:
+                line['placement']['selection'] = dict(
+                    candidates=len(probe_ms) or 1, by='probe', probe_ms=probe_ms or None,
+                    note='the timed trajectory is the fastest of the candidate allocations under the placement probe '
+                         '(cs_traj_probe: the rollout\'s writes, zeros, no game logic; DESIGN 7), chosen before '
+                         'warm-up')
         line.update(gather_info)
         if philox_info is not None:
             line['rng_philox'] = philox_info

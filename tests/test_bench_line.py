@@ -49,5 +49,6 @@ def test_bench_line_on_the_gpu():
     wp = r['write_probe']
     assert wp['ms'] > 0 and wp['bytes'] > 0 and wp['kernel_over_probe'] > 0
     sel = d['placement']['selection']
-    assert sel['candidates'] == 2 and len(sel['probe_ms']) == 2
+    assert sel['candidates'] == 2 and sel['by'] == 'rollout' and len(sel['rollout_ms']) == 2
+    assert r['kernel_ms_per_launch'] < 1.5 * min(sel['rollout_ms']) + 0.05
     assert len(d['placement']['kernel_ms_per_allocation']) == 2
