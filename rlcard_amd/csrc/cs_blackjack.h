@@ -27,25 +27,7 @@
 // uses to collect the 51 draws (per-lane byte positions) before they move to registers.
 #pragma once
 #include "cs_device.h"
-
-// MT staging rows of 128 bytes: the reset's ~57 draws come out of one branch-free pass over them
-// (RingLane::draw_intervals); measured 17.2 ms per 2^20 x 64 launch vs 19.9 with 64-byte rows (3 waves per SIMD
-// instead of 2, but more draws past the row) and 35.0 with 256-byte rows (1 wave); R 72..112 the same
-#ifndef CS_BJ_STAGE_W
-#define CS_BJ_STAGE_W 128
-#endif
-#ifndef CS_BJ_STAGE_R
-#define CS_BJ_STAGE_R 100
-#endif
-#ifndef CS_BJ_RESTAGE_B
-#define CS_BJ_RESTAGE_B 8   // measured with 128-byte rows: 8 > 4 > 1
-#endif
-#ifndef CS_BJ_MIN_WAVES
-#define CS_BJ_MIN_WAVES 3   // the LDS (stage rows + scratch) allows 3 blocks of 4 waves per CU
-#endif
-#ifndef CS_BJ_SWAR_DEAL
-#define CS_BJ_SWAR_DEAL 1   // 0: the initial deal traces its positions one at a time (A/B knob, same cards)
-#endif
+#include "cs_prof.h"
 
 namespace cs {
 
@@ -59,9 +41,12 @@ struct Blackjack {
     static constexpr int HAND_W = 3 * (NP + 1);                 // state words 15.. the hands use
     static constexpr int SCRATCH_WORDS = 3 + HAND_W > 13 ? 3 + HAND_W : 13;   // >= 13: the reset's draw bytes
     // MT staging (see MtLaneT)
-    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = CS_BJ_STAGE_W, STAGE_PAD = 8, STAGE_R = CS_BJ_STAGE_R;
-    static constexpr int RESTAGE_B = CS_BJ_RESTAGE_B;  // row loads in flight per lane and restage pass
-    static constexpr int MIN_WAVES = CS_BJ_MIN_WAVES;
+    // MT staging rows of 128 bytes: the reset's ~57 draws come out of one branch-free pass over them
+    // (RingLane::draw_intervals); measured 17.2 ms per 2^20 x 64 launch vs 19.9 with 64-byte rows (3 waves per SIMD
+    // instead of 2, but more draws past the row) and 35.0 with 256-byte rows (1 wave); R 72..112 the same
+    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_PAD = 8, STAGE_R = 100;
+    static constexpr int RESTAGE_B = 8;   // row loads in flight per lane and restage pass (128-byte rows: 8 > 4 > 1)
+    static constexpr int MIN_WAVES = 3;   // the LDS (stage rows + scratch) allows 3 blocks of 4 waves per CU
     static constexpr int EPW = 64;        // rollout envs per wave (lane_ctx)
     static constexpr int REFILL_K = 2;   // stale blocks twisted per pass (see mt_refill_wave)
 
@@ -200,7 +185,7 @@ struct Blackjack {
     // the card at final deck position x: undo the swaps from the last (i = 1) to the first (i = 51)
     __device__ __forceinline__ int card_at(int x) const
     {
-#ifdef CS_PROF_BJ_NOTRACE   // profiling builds only: wrong cards, timing of the swap trace-back
+#if CS_PROF_BJ_NOTRACE   // profiling builds only (cs_prof.h)
         return x;
 #endif
         // the draws pass through an empty asm: opaque values, so the compiler cannot hoist the 51 extracted draws out
@@ -224,7 +209,7 @@ struct Blackjack {
     template <int NW>
     __device__ __forceinline__ void cards_at(uint32_t (&X)[NW]) const
     {
-#ifdef CS_PROF_BJ_NOTRACE
+#if CS_PROF_BJ_NOTRACE
         return;
 #endif
 #pragma unroll
@@ -295,22 +280,19 @@ struct Blackjack {
         for (int w = 0; w < 13; w++) jw[w] = L(w);
         jw[12] &= 0xFFFFFFu;   // byte 51: no draw
         clear_table();
+        // every dealt position first (they depend only on the stream and the removed set), traced back together
         constexpr int ND = 2 * (NP + 1), NW = (ND + 3) / 4;
-        if constexpr (CS_BJ_SWAR_DEAL) {
-            uint32_t X[NW];
+        uint32_t X[NW];
 #pragma unroll
-            for (int w = 0; w < NW; w++) X[w] = 0x3F3F3F3Fu;
+        for (int w = 0; w < NW; w++) X[w] = 0x3F3F3F3Fu;
 #pragma unroll
-            for (int d = 0; d < ND; d++) {
-                const uint32_t sh = 8u * (uint32_t)(d & 3);
-                X[d >> 2] = (X[d >> 2] & ~(255u << sh)) | (uint32_t)deal_pos(rng) << sh;
-            }
-            cards_at(X);
-#pragma unroll
-            for (int d = 0; d < ND; d++) add_card(d % (NP + 1), (int)((X[d >> 2] >> (8 * (d & 3))) & 255u));
-        } else {
-            for (int d = 0; d < ND; d++) deal(rng, d % (NP + 1));
+        for (int d = 0; d < ND; d++) {
+            const uint32_t sh = 8u * (uint32_t)(d & 3);
+            X[d >> 2] = (X[d >> 2] & ~(255u << sh)) | (uint32_t)deal_pos(rng) << sh;
         }
+        cards_at(X);
+#pragma unroll
+        for (int d = 0; d < ND; d++) add_card(d % (NP + 1), (int)((X[d >> 2] >> (8 * (d & 3))) & 255u));
     }
 
     template <class Rng>

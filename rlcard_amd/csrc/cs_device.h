@@ -15,52 +15,23 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "cs_prof.h"
+
 namespace cs {
 
 // rollout output stores: nontemporal (streamed past the caches: written once, GBs per launch, read by the consumer
-// long after), measured faster than default-policy stores (Leduc 2.37 -> 2.08 ms, Limit 1.39 -> 1.33 ms per launch);
-// CS_OUT_NT=0 for A/B runs
-#ifndef CS_OUT_NT
-#define CS_OUT_NT 1
-#endif
+// long after), measured faster than default-policy stores (Leduc 2.37 -> 2.08 ms, Limit 1.39 -> 1.33 ms per launch)
+// and than explicit gfx950 cache-policy bits (round 5, profiles/EXPERIMENTS.md)
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-// CS_OUT_CPOL (A/B builds only): the 16-B trajectory stores as inline-asm global_store_dwordx4 with these gfx950 cache
-// policy bits (e.g. "sc1", "nt sc1", "sc0 sc1"); the compiler does not count an asm store in its vmcnt bookkeeping,
-// which only makes its later waits longer (the counter is in order), never short
 __device__ __forceinline__ void out_store16(uint4* p, const uint4& v)
 {
-#if defined(CS_OUT_CPOL_SEL) && !defined(CS_OUT_CPOL)
-#if CS_OUT_CPOL_SEL == 1
-#define CS_OUT_CPOL "sc1"
-#elif CS_OUT_CPOL_SEL == 2
-#define CS_OUT_CPOL "nt sc1"
-#elif CS_OUT_CPOL_SEL == 3
-#define CS_OUT_CPOL "sc0 sc1"
-#elif CS_OUT_CPOL_SEL == 4
-#define CS_OUT_CPOL "sc0"
-#else
-#define CS_OUT_CPOL ""
-#endif
-#endif
-#ifdef CS_OUT_CPOL
-    {
-        const u32x4_t x = {v.x, v.y, v.z, v.w};
-        asm volatile("global_store_dwordx4 %0, %1, off " CS_OUT_CPOL : : "v"(p), "v"(x) : "memory");
-        return;
-    }
-#endif
-    if constexpr (CS_OUT_NT) {
-        const u32x4_t x = {v.x, v.y, v.z, v.w};
-        __builtin_nontemporal_store(x, (u32x4_t*)p);
-    } else {
-        *p = v;
-    }
+    const u32x4_t x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, (u32x4_t*)p);
 }
 template <class T>
 __device__ __forceinline__ void out_store(T* p, T v)
 {
-    if constexpr (CS_OUT_NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
+    __builtin_nontemporal_store(v, p);
 }
 
 constexpr int MT_N = 624;

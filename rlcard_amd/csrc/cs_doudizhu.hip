@@ -26,23 +26,13 @@
 namespace cs {
 namespace ddz {
 
-#ifndef CS_DDZ_BLOCK
-#define CS_DDZ_BLOCK 256
-#endif
-#ifndef CS_DDZ_MINW
-#define CS_DDZ_MINW 1   // k_rollout: minimum waves per SIMD the register allocation must allow (6 forces 80 VGPRs: slower)
-#endif
-constexpr int BLOCK = CS_DDZ_BLOCK;
+constexpr int BLOCK = 256;                        // the one-env kernels (reset / step / observe / debug)
 constexpr int WPB = BLOCK / WAVE;
 constexpr int MASK_PAD = 4;                       // zero dwords on both sides of the mask image
 constexpr int KTH_LANES = 54, KTH_WORDS = 16;     // kth_legal: lane l scans mask dwords [16 l, 16 l + 16)
 constexpr int MASK_WORDS = MASK_PAD + KTH_LANES * KTH_WORDS + MASK_PAD;
 constexpr int NSEG = 20;                          // 54-bit obs blocks (16 used) + zero tail
 constexpr int BV_WORDS = 32;                      // obs bits (912 + 16 front pad) as dwords
-#ifndef CS_PROF_DDZ
-#define CS_PROF_DDZ 0   // profiling only (wrong outputs): 32 no table loads in the legal build, 1 skip legal rows, 2 skip obs rows, 4 skip build_obs (one-env
-                        // kernels), 16 skip build_obs2 (pair kernel)
-#endif
 
 constexpr int LIST_RING = 128;                    // the step's tested mask dwords (a ring: see build_legal)
 constexpr int LIST_CAP = 64;                      // kth_legal reads the list when it holds them all, one per lane
@@ -210,15 +200,15 @@ struct Cand {
                (r_len && r_lo < hi && r_lo + r_len > lo);
     }
 };
-__device__ __forceinline__ Cand cand_of(const Env& e, const Tab& tb, const TabLds& T)
+__device__ __forceinline__ Cand cand_at(uint32_t greater, uint32_t cur, uint32_t ggrp, const Tab& tb, const TabLds& T)
 {
     Cand c;
-    c.leading = e.greater == NONE || e.greater == e.cur;   // player.py:60-86 available_actions
+    c.leading = greater == NONE || greater == cur;   // player.py:60-86 available_actions
     if (c.leading) {
         c.c_lo = 0; c.c_len = PASS; c.b_lo = 0; c.b_len = 0; c.r_lo = 0; c.r_len = 0;
         return c;
     }
-    const uint4 q = T.grp[e.ggrp];
+    const uint4 q = T.grp[ggrp];
     const uint32_t z = q.z, y = q.w;
     const uint32_t gend = z >> 16, tend = y & 0xFFFFu, type = (y >> 16) & 0xFFu;
     if (type == (uint32_t)TYPE_ROCKET) {
@@ -232,6 +222,10 @@ __device__ __forceinline__ Cand cand_of(const Env& e, const Tab& tb, const TabLd
     c.r_lo = (uint32_t)tb.rocket;
     c.r_len = 1;
     return c;
+}
+__device__ __forceinline__ Cand cand_of(const Env& e, const Tab& tb, const TabLds& T)
+{
+    return cand_at(e.greater, e.cur, e.ggrp, tb, T);
 }
 
 // single-id legality + the fallback for an id outside the legal set (cs_step only; the reference has no decode
@@ -389,8 +383,7 @@ __device__ __forceinline__ void test_listed(uint32_t t0, uint32_t nl, uint64_t h
         dw[q] = ent[q] ? L.lst[e & (LIST_RING - 1)] : 0u;
         id[q] = dw[q] * 32u + (uint32_t)(lane & 31);
         live[q] = ent[q] && id[q] < (uint32_t)PASS;
-        if constexpr ((CS_PROF_DDZ & 32) != 0) cnt[q] = live[q] ? simple_cnt(id[q], (uint32_t)tb.bomb_lo) : ~0ull;   // profiling
-        else cnt[q] = live[q] ? tb.cnt[id[q]] : ~0ull;
+        cnt[q] = live[q] ? tb.cnt[id[q]] : ~0ull;
     }
 #pragma unroll
     for (int q = 0; q < PAIRS; q++) {
@@ -670,12 +663,13 @@ __device__ __forceinline__ void emit_state(const Env& e, uint32_t self, const Ta
     }
 }
 
-__device__ __forceinline__ void payoffs(const Env& e, float* r)   // judger.py:350-359
+__device__ __forceinline__ void payoffs(uint32_t winner, float* r)   // judger.py:350-359
 {
-    r[0] = e.winner == 0 ? 1.f : 0.f;
-    r[1] = e.winner == 0 ? 0.f : 1.f;
+    r[0] = winner == 0 ? 1.f : 0.f;
+    r[1] = winner == 0 ? 0.f : 1.f;
     r[2] = r[1];
 }
+__device__ __forceinline__ void payoffs(const Env& e, float* r) { payoffs(e.winner, r); }
 
 template <bool PHX>
 __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n,
@@ -762,129 +756,53 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n
     }
 }
 
-template <bool PHX>
-__global__ __launch_bounds__(BLOCK, CS_DDZ_MINW) void k_rollout(uint32_t* mt, uint32_t* ctl, uint32_t* st, int64_t n, int T,
-                                                    uint64_t seed, uint64_t t0, uint64_t env_base, cs_traj_out out,
-                                                    Tab tb)
-{
-    __shared__ WaveLds lds[WPB];
-    __shared__ TabLds tl;
-    load_tab(tl, tb);                 // every thread of the block, before any wave leaves
-    const Ctx c = ctx_of(n);
-    if (!c.valid) return;
-    WaveLds& L = lds[c.wid];
-    const int lane = c.lane;
-    Env e;
-    e.load(st, c.env, lane, tb);
-    auto m = wave_mt<PHX>(mt, ctl, c.env);
-    if (e.over()) deal(e, m, lane);
-    const uint64_t genv = env_base + (uint64_t)c.env;
-    uint32_t rr_lane = 0;
-    for (int t = 0; t < T; t++) {
-        const int64_t row = (int64_t)t * n + c.env;
-        zero_mask(L, lane);
-        wave_sync_lds();
-        const Cand cd = cand_of(e, tb, tl);
-        const Legal lg = build_legal(e, cd, tb, tl, L, lane);
-        if (!(CS_PROF_DDZ & 4)) build_obs(e, e.cur, L, lane);
-        wave_sync_lds();
-        const uint32_t count = lg.total + (cd.leading ? 0u : 1u);
-        // the policy draws of 64 steps at once, one per lane (vector ALU; the scalar unit is the busy one)
-        if ((t & (WAVE - 1)) == 0) rr_lane = philox_u32(seed, genv, t0 + (uint64_t)(t + lane));
-        const uint32_t rr = rl(rr_lane, t & (WAVE - 1));
-        const uint32_t a = kth_legal((uint32_t)(((uint64_t)rr * count) >> 32), lg, L, lane);
-        if (!cd.leading && lane == 0) L.mask[MASK_PAD + PASS / 32] |= 1u << (PASS & 31);
-        wave_sync_lds();
-        write_rows(L, (CS_PROF_DDZ & 2) ? nullptr : (uint8_t*)out.obs + row * OBS,
-                   (CS_PROF_DDZ & 1) ? nullptr : (uint8_t*)out.legal + row * LB, lane);
-        const uint32_t p = e.cur;
-        e.apply(a, tb, lane);
-        const bool done = e.over();
-        if (lane == 0) {
-            ((uint8_t*)out.player)[row] = (uint8_t)p;
-            ((int16_t*)out.action)[row] = (int16_t)a;
-            float r[3] = {0.f, 0.f, 0.f};
-            if (done) payoffs(e, r);
-            float* o = (float*)out.reward + row * P;
-            o[0] = r[0]; o[1] = r[1]; o[2] = r[2];
-            ((uint8_t*)out.done)[row] = (uint8_t)done;
-        }
-        if (done) {
-            if (out.final_obs) {   // Env.run's final state of every player (envs/env.py:161-164)
-                for (uint32_t q = 0; q < (uint32_t)P; q++) {
-                    wave_sync_lds();
-                    build_obs(e, q, L, lane);
-                    wave_sync_lds();
-                    write_rows(L, (uint8_t*)out.final_obs + (row * P + q) * OBS, nullptr, lane);
-                }
-            }
-            deal(e, m, lane);
-        }
-    }
-    e.store(st, c.env, lane);
-    if (lane == 0) m.save(ctl, c.env);
-}
-
-// ---- the rollout with TWO envs per wave ---------------------------------------------------------------------------
+// ---- the rollout: TWO envs per wave, legal rows without a mask image ------------------------------------------------
 // Lanes 0..31 play one env and lanes 32..63 the next: every step below runs for both envs in the same instructions
 // (each half-wave is one env's 32 lanes), so the game logic that the one-env kernels run as wave-uniform scalar code
 // -- the scalar unit is their busiest pipe -- becomes vector code shared by two envs, and the two envs' dependency
 // chains (LDS round trips, table loads) overlap inside one wave. Same functions of the same state, same outputs:
 // the per-env values are simply held per lane (uniform within a half). The deal (rare: once per game) still runs with
 // the whole wave for one env at a time, through the one-env `deal`.
-#ifndef CS_DDZ_PAIR
-#define CS_DDZ_PAIR 1
-#endif
+//
+// The legal row is 27 472 bits of which a random-play step sets ~6 (1.8 nonzero mask dwords on average, at most 46 in
+// 409 600 steps of random play, `tools/ddz_sparsity.py`). So the step keeps no 3.4 KB mask image: the legal scan
+// appends each nonzero mask dword (index, value) to a list in ascending order (NZ_CAP entries, a bitmap of the listed
+// dwords and its prefix ranks), the policy pick scans the list's popcounts, and the row's 16-B chunks are zeros except
+// where the bitmap says a listed dword falls -- those few are gathered from the list. Per env 1.6 KB of LDS instead of
+// 4.4 KB, no per-step zeroing or cleaning of an image. A step whose list overflows (more than NZ_CAP nonzero dwords:
+// none seen in random play, but a 20-card hand can have hundreds) runs the legal scan a second time with a row cursor
+// that writes the row in ascending order straight to HBM (zeros between the nonzero dwords) and finds the picked id on
+// the way; kernel flag bit 1 forces that path for every step (tests/test_gpu_engine.py runs it against the oracle).
 #ifndef CS_DDZ_PAIR_WAVES
-#define CS_DDZ_PAIR_WAVES 8   // waves per block: the group table in LDS is shared by 16 envs
-#endif
-#ifndef CS_DDZ_LROW_UNROLL
-#define CS_DDZ_LROW_UNROLL 4  // legal-row chunk loads in flight (unrolled iterations of 32 lanes per env)
+#define CS_DDZ_PAIR_WAVES 4   // waves per block (the group table in LDS is shared by 2 x this many envs)
 #endif
 #ifndef CS_DDZ_PAIR_MINW
-#define CS_DDZ_PAIR_MINW 4    // waves per SIMD the registers must allow (LDS allows 4: two 79-KB blocks per CU)
+#define CS_DDZ_PAIR_MINW 5    // waves per SIMD the registers must allow
 #endif
 constexpr int HW = WAVE / 2;                         // lanes per env
 constexpr int PWPB = CS_DDZ_PAIR_WAVES, PBLOCK = PWPB * WAVE;
-constexpr int NCH = (ND + HW - 1) / HW;              // 27 chunks of 32 mask dwords
-// The pair kernel keeps the legal mask image SHIFTED by the legal row's misalignment mis (row byte o at image byte
-// 16 + mis + o), so the row's 16-B chunks are aligned 16-B blocks of the image (ds_read_b128, no bank conflicts, no
-// byte alignment); a mask dword is written / read at byte 16 + mis + 4 d (2-byte aligned: mis is even).
-// the image padded to whole 16-B stores of 32 lanes: the per-step zeroing runs unpredicated, so every store takes the
-// same zero register (predicated, the compiler kept a second zero in a scratch spill whose reload waited on vmcnt(0)
-// -- every row store of the previous step -- at the top of each step)
-#ifndef CS_DDZ_PAD
-#define CS_DDZ_PAD 1
-#endif
-#ifndef CS_DDZ_SIMPLE
-#define CS_DDZ_SIMPLE 1   // bit 0: the fast path's candidates, bit 1: the chosen action's entries from simple_cnt / _gid (bit 1 measured 11 % slower: the select puts the table load's wait before the row stores)
-#endif
-#ifndef CS_DDZ_XCD
-#define CS_DDZ_XCD 1   // k_rollout2 blocks in XCD-aware order (cs_device.h xcd_block): rows shared by neighbouring blocks
-                       // meet in one L2
-#endif
-#ifndef CS_DDZ_ROWSTRIDE_L   // profiling builds only (tools/place_probe3.py PP_PAD): rows written at a padded stride
-#define CS_DDZ_ROWSTRIDE_L LB
-#endif
-#ifndef CS_DDZ_ROWSTRIDE_O
-#define CS_DDZ_ROWSTRIDE_O OBS
-#endif
-#ifndef CS_DDZ_CLEAN
-#define CS_DDZ_CLEAN 1   // zero only the dwords a step wrote, after its row is out (full zeroing when the list wrapped)
-#endif
-constexpr int PMASK_WORDS = CS_DDZ_PAD ? (MASK_WORDS / 4 + HW - 1) / HW * HW * 4 : MASK_WORDS;
+constexpr int NCH = (ND + HW - 1) / HW;              // 27 chunks of 32 mask dwords (pass b of the legal scan)
+constexpr int NZ_CAP = 64;                           // nonzero mask dwords an env's list holds
+constexpr int TRING = 64;                            // pass c's ring of dwords waiting for their test (<= 3 + 32)
+constexpr int NZBM = 28;                             // bitmap words over the 859 mask dwords, + 1 zero word
+constexpr int LROW_IT = (LB + 15 + 15) / 16 / HW + 1;   // 32-lane iterations over a legal row's <= 216 16-B chunks
 struct alignas(16) PairLds {
-    uint32_t mask[PMASK_WORDS];                      // the shifted image (see above)
-    union {
-        uint16_t pre[MAX_GROUPS + 8];                // the legal scan's group prefix counts, dead once it is done:
-        struct {                                     // the obs image reuses the space
-            uint64_t segv[NSEG];
-            uint32_t bv[BV_WORDS];
-        } o;
-    } u;
-    uint16_t lst[LIST_RING];
+    uint32_t val[NZ_CAP];            // the step's nonzero mask dwords in ascending order: values
+    uint32_t nzbm[NZBM];             // bit d: mask dword d is in the list
+    uint16_t idx[NZ_CAP];            //   ... their indices
+    uint16_t tst[TRING];             // pass c's ring of dwords to test / the following fast path's OR scratch
+    uint16_t pre[MAX_GROUPS + 8];    // pass a's group prefix counts
+    uint8_t npre[32];                // listed dwords before bitmap word w
+    uint64_t segv[NSEG];             // the obs image: 54-bit blocks
+    uint32_t bv[BV_WORDS];           //   ... and its bits (obs bit x at bit 16 + x)
+    uint64_t q[3];                   // the env's played cards (Round.played_cards): read by the obs, added to by a play
+    // cold env state, touched at a deal and at the end of the launch only
+    uint64_t mkey;                   // the stream (WaveMt fields): Philox key,
+    uint32_t mpos, mdabs;            //   position | stale << 16, Philox draw count
+    uint8_t deck[64];                // the dealt deck (state words W_DECK..)
 };
-static_assert(MAX_GROUPS % HW == 0 && NSEG <= HW && BV_WORDS == HW && NCH <= HW, "pair layout");
+static_assert(MAX_GROUPS % HW == 0 && NSEG <= HW && BV_WORDS == HW && NCH <= HW && NZBM <= HW && NZ_CAP <= 2 * HW &&
+              (ND + 31) / 32 < NZBM && 2 * TRING >= 4 * HW, "pair layout");
 
 __device__ __forceinline__ uint32_t half32(uint64_t b, int lane) { return lane < HW ? (uint32_t)b : (uint32_t)(b >> 32); }
 __device__ __forceinline__ uint32_t below32(uint32_t m, int hl) { return (uint32_t)__popc(m & ((1u << hl) - 1u)); }
@@ -898,17 +816,78 @@ __device__ __forceinline__ uint64_t hshfl64(uint64_t v, int lane, uint32_t k)
     return (uint64_t)hshfl((uint32_t)v, lane, k) | ((uint64_t)hshfl((uint32_t)(v >> 32), lane, k) << 32);
 }
 
-// mask dword d of the shifted image (byte 16 + mis + 4 d: mis even, so 4- or 2-byte aligned)
-__device__ __forceinline__ void put_mask(PairLds& L, uint32_t d, uint32_t mis, uint32_t v)
+// An env held by a half-wave: every field uniform within the half (per lane), the small fields packed, the trace's
+// last 9 entries distributed over lanes 3..11 (like Env::hcnt) -- the registers the step loop keeps live
+struct PEnv {
+    uint64_t h0, h1, h2;   // hands (the played cards are in the env's LDS, PairLds::q)
+    uint64_t hcnt;         // lane s = 3..11: packed counts of trace entry s - 3 of the last 9 (0: pass / none)
+    uint32_t hid;          // lane s = 3..11: its action id (NO_ACTION: none)
+    uint32_t gw;           // greater player's last play id | its (type, weight) group << 16
+    uint32_t sw;           // ntrace | greater << 16 | cur << 20 | winner << 24 (players and NONE fit 2 bits)
+    __device__ __forceinline__ uint32_t ntrace() const { return sw & 0xFFFFu; }
+    __device__ __forceinline__ uint32_t greater() const { return (sw >> 16) & 3u; }
+    __device__ __forceinline__ uint32_t cur() const { return (sw >> 20) & 3u; }
+    __device__ __forceinline__ uint32_t winner() const { return (sw >> 24) & 3u; }
+    __device__ __forceinline__ uint32_t ggrp() const { return gw >> 16; }
+    __device__ __forceinline__ bool over() const { return winner() != NONE; }
+    __device__ __forceinline__ uint64_t hand(uint32_t p) const
+    {
+        return keep64(p == 0, h0) | keep64(p == 1, h1) | keep64(p == 2, h2);
+    }
+    // Env::apply_with for the half's env (hl: lane in the half; q: its played cards)
+    __device__ __forceinline__ void apply_with(uint32_t a, uint64_t c, uint32_t gid, int hl, uint64_t* q)
+    {
+        const uint32_t p = cur();
+        const uint64_t down = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)hcnt, 1) |
+                              ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(hcnt >> 32), 1) << 32);
+        const uint32_t hdown = (uint32_t)__shfl_down((int)hid, 1);
+        const bool mid = hl >= 3 && hl < 11;
+        hcnt = hl == 11 ? c : (mid ? down : 0ull);
+        hid = hl == 11 ? a : (mid ? hdown : NO_ACTION);
+        uint32_t s = sw + 1u;   // ntrace++
+        if (a != (uint32_t)PASS) {
+            const uint64_t c0 = keep64(p == 0, c), c1 = keep64(p == 1, c), c2 = keep64(p == 2, c);
+            h0 -= c0; h1 -= c1; h2 -= c2;
+            if (hl == 0) q[p] += c;
+            gw = a | gid << 16;
+            s = (s & ~(3u << 16)) | p << 16;
+            if (hand(p) == 0) s = (s & ~(3u << 24)) | p << 24;
+        }
+        s &= ~(3u << 20);
+        sw = s | (p == 2 ? 0u : p + 1u) << 20;
+    }
+};
+
+// cand_of for a half's env: the same type's greater weights [c_lo, c_lo + c_len) (leading: every id), the bombs and
+// the rocket as flags over the table's ranges (scalars)
+struct PCand {
+    uint32_t c_lo, c_len;
+    uint32_t fl;              // bit 0: the bombs, bit 1: the rocket, bit 2: leading
+    uint32_t b_lo, b_n, r_lo; // the table's bomb range and rocket id
+    __device__ __forceinline__ bool leading() const { return (fl & 4u) != 0u; }
+    __device__ __forceinline__ uint32_t nb() const { return (fl & 1u) ? b_n : 0u; }
+    __device__ __forceinline__ uint32_t nr() const { return (fl >> 1) & 1u; }
+    __device__ __forceinline__ bool ok(uint32_t x) const
+    {
+        return (x - c_lo < c_len) | ((fl & 1u) && x - b_lo < b_n) | ((fl & 2u) && x == r_lo);
+    }
+    __device__ __forceinline__ bool meets(uint32_t lo, uint32_t hi) const   // does a candidate lie in [lo, hi)?
+    {
+        return (c_len && c_lo < hi && c_lo + c_len > lo) | ((fl & 1u) && b_lo < hi && b_lo + b_n > lo) |
+               ((fl & 2u) && r_lo < hi && r_lo >= lo);
+    }
+};
+__device__ __forceinline__ PCand pcand(const PEnv& e, const Tab& tb, const TabLds& T)
 {
-    uint16_t* h = (uint16_t*)L.mask + ((16u + mis + 4u * d) >> 1);   // two 16-bit stores: no branch on the alignment
-    h[0] = (uint16_t)v;
-    h[1] = (uint16_t)(v >> 16);
-}
-__device__ __forceinline__ uint32_t get_mask(const PairLds& L, uint32_t d, uint32_t mis)
-{
-    const uint32_t b = 16u + mis + 4u * d;
-    return __builtin_amdgcn_alignbyte(L.mask[(b >> 2) + 1], L.mask[b >> 2], b & 3u);
+    const Cand c = cand_at(e.greater(), e.cur(), e.ggrp(), tb, T);
+    PCand p;
+    p.c_lo = c.c_lo;
+    p.c_len = c.c_len;
+    p.fl = (c.b_len ? 1u : 0u) | (c.r_len ? 2u : 0u) | (c.leading ? 4u : 0u);
+    p.b_lo = (uint32_t)tb.bomb_lo;
+    p.b_n = (uint32_t)(tb.bomb_hi - tb.bomb_lo);
+    p.r_lo = (uint32_t)tb.rocket;
+    return p;
 }
 
 // inclusive prefix sum within each half-wave, with DPP (no LDS): row_shr 1, 2, 4, 8 inside the 16-lane rows, then
@@ -923,9 +902,74 @@ __device__ __forceinline__ uint32_t scan32(uint32_t x)
     return x;
 }
 
+// the k-th set bit of each half's `m` (k < popcount(m), per half)
+__device__ __forceinline__ uint32_t kth_bit32(uint32_t m, uint32_t k, int lane)
+{
+    const int hl = lane & (HW - 1);
+    const uint32_t bm = half32(__ballot(((m >> hl) & 1u) && below32(m, hl) == k), lane);
+    return bm ? (uint32_t)__builtin_ctz(bm) : 0u;
+}
+
+// ---- the sinks of the legal scan: where each tested mask dword's value goes (in ascending dword order) -------------
+// the list (the usual path): nonzero dwords appended with their bitmap bit; n counts past NZ_CAP (overflow)
+struct NzSink {
+    PairLds* L;
+    uint32_t n;   // per half
+    __device__ __forceinline__ void operator()(bool ent, uint32_t dw, uint32_t m, int lane)
+    {
+        const bool put = ent && m != 0u;
+        if (put && (lane & (HW - 1)) == 0 && n < (uint32_t)NZ_CAP) {
+            L->val[n] = m;
+            L->idx[n] = (uint16_t)dw;
+            atomicOr(&L->nzbm[dw >> 5], 1u << (dw & 31u));
+        }
+        n += put ? 1u : 0u;
+    }
+};
+// the overflow path: the row written in ascending order straight to HBM (u16 stores: rows start at even addresses),
+// zeros between the nonzero dwords, and the k-th legal id found on the way
+struct RowCursor {
+    uint8_t* row;      // per half; null: the half is not on this path
+    uint32_t w;        // row bytes written
+    uint32_t k, run;   // the pick: the k-th legal id (k < the legal count), legal ids seen so far
+    uint32_t found;
+    bool pass;         // the pass bit goes into dword ND - 1 (its bit PASS % 32)
+    __device__ __forceinline__ void fill(uint32_t to, int lane)   // zeros over [w, to), both even
+    {
+        uint32_t o = w + 2u * (uint32_t)(lane & (HW - 1));
+        while (__ballot(row != nullptr && o < to)) {
+            if (row != nullptr && o < to) *(uint16_t*)(row + o) = 0;
+            o += 2u * HW;
+        }
+        if (row != nullptr) w = to > w ? to : w;
+    }
+    __device__ __forceinline__ void put(bool ent, uint32_t dw, uint32_t m, int lane)
+    {
+        const bool on = row != nullptr && ent && (m != 0u || (pass && dw == (uint32_t)(ND - 1)));
+        const uint32_t c = (uint32_t)__popc(m);
+        const uint32_t kb = kth_bit32(m, k - run, lane);
+        if (on && k >= run && k < run + c) found = dw * 32u + kb;
+        run += on ? c : 0u;
+        const uint32_t v = m | (pass && dw == (uint32_t)(ND - 1) ? 1u << (PASS & 31) : 0u);
+        fill(on ? 4u * dw : 0u, lane);
+        if (on && (lane & (HW - 1)) == 0) {
+            *(uint16_t*)(row + 4u * dw) = (uint16_t)v;
+            if (4u * dw + 2u < (uint32_t)LB) *(uint16_t*)(row + 4u * dw + 2u) = (uint16_t)(v >> 16);
+        }
+        if (on) w = 4u * dw + 4u < (uint32_t)LB ? 4u * dw + 4u : (uint32_t)LB;
+    }
+    __device__ __forceinline__ void operator()(bool ent, uint32_t dw, uint32_t m, int lane) { put(ent, dw, m, lane); }
+    __device__ __forceinline__ void finish(int lane)   // the pass dword if no tested dword carried it, the zero tail
+    {
+        put(pass && w <= 4u * (uint32_t)(ND - 1), (uint32_t)(ND - 1), 0u, lane);
+        fill((uint32_t)LB, lane);
+    }
+};
+
 // pass c (see build_legal) for the listed dwords [t0, lim) of each half's env, up to 4 per env
-__device__ __forceinline__ void test_listed2(uint32_t t0, uint32_t lim, uint64_t h, const Cand& c, const Tab& tb,
-                                             PairLds& L, uint32_t mis, int lane, Legal& r)
+template <class Sink>
+__device__ __forceinline__ void test_listed2(uint32_t t0, uint32_t lim, uint64_t h, const PCand& c, const Tab& tb,
+                                             const PairLds& L, int lane, Legal& r, Sink& sink)
 {
     const int hl = lane & (HW - 1);
     uint64_t cnt[4];
@@ -935,16 +979,15 @@ __device__ __forceinline__ void test_listed2(uint32_t t0, uint32_t lim, uint64_t
     for (int q = 0; q < 4; q++) {
         const uint32_t e = t0 + (uint32_t)q;
         ent[q] = e < lim;
-        dw[q] = ent[q] ? L.lst[e & (LIST_RING - 1)] : 0u;
+        dw[q] = ent[q] ? L.tst[e & (TRING - 1)] : 0u;
         id[q] = dw[q] * 32u + (uint32_t)hl;
         live[q] = ent[q] && id[q] < (uint32_t)PASS;
-        if constexpr ((CS_PROF_DDZ & 32) != 0) cnt[q] = live[q] ? simple_cnt(id[q], (uint32_t)tb.bomb_lo) : ~0ull;   // profiling
-        else cnt[q] = live[q] ? tb.cnt[id[q]] : ~0ull;
+        cnt[q] = live[q] ? tb.cnt[id[q]] : ~0ull;
     }
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const uint32_t m = half32(__ballot(live[q] && contains(h, cnt[q]) && c.ok(id[q])), lane);
-        if (hl == 0 && ent[q]) put_mask(L, dw[q], mis, m);
+        sink(ent[q], dw[q], m, lane);
         r.total += (uint32_t)__popc(m);
     }
 }
@@ -953,46 +996,40 @@ __device__ __forceinline__ void test_listed2(uint32_t t0, uint32_t lim, uint64_t
 // rocket). In random play they number <= 32 in ~93 % of the following steps (~70 % of all steps; the same-type range
 // has median 5 ids, p90 14), and then the half's 32 lanes test one candidate each -- no group pass, no chunk pass, no
 // listed-dword batches. Lane k takes the k-th candidate in id order (the table's bomb and rocket types are its last
-// ids, so the ranges come in the order same type < bombs < rocket); the dwords holding a legal id are listed in order
-// (the group path lists every dword it tests; kth_legal2 only sums their popcounts) and the legal bits OR-ed into the
-// shifted image through 32 scratch dwords (the upper half of the list: this path lists at most 32 dwords). Same image,
-// same legal count. Two parts: fast_issue loads the candidates' packed counts from the table in HBM / L2 at the start
-// of the step, fast_finish tests them after the group pass (other half) and build_obs2, which hide the load latency
-// (issued and tested back to back the path measured slower than the group pass it replaces). The solo / pair / trio /
-// bomb / rocket candidates (~95 % of these steps have no other) take their counts from simple_cnt: no load.
-#ifndef CS_DDZ_FAST_FOLLOW
-#define CS_DDZ_FAST_FOLLOW 1
-#endif
+// ids, so the ranges come in the order same type < bombs < rocket); the dwords holding a legal id go to the list in
+// order, their bits OR-ed together through 32 scratch dwords. Two parts: fast_issue loads the candidates' packed counts
+// from the table in HBM / L2 at the start of the step, fast_finish tests them after the group pass (other half) and
+// build_obs2, which hide the load latency (issued and tested back to back the path measured slower than the group pass
+// it replaces). The solo / pair / trio / bomb / rocket candidates (~95 % of these steps have no other) take their
+// counts from simple_cnt: no load. Kernel flag bit 0 turns the path off (the group pass for every step: same outputs).
 struct Fast {
     bool fast, cand, load;   // load: a candidate that is not a simple id (its counts come from the table)
     uint32_t id;
     uint64_t cnt;
 };
-__device__ __forceinline__ Fast fast_issue(const Env& e, const Cand& c, const Tab& tb, PairLds& L, int lane, bool act)
+__device__ __forceinline__ Fast fast_issue(const PEnv& e, const PCand& c, const Tab& tb, PairLds& L, int lane, bool act)
 {
     const uint32_t hl = (uint32_t)(lane & (HW - 1));
     Fast f;
-    f.fast = CS_DDZ_FAST_FOLLOW != 0 && act && !e.over() && !c.leading && c.c_len + c.b_len + c.r_len <= (uint32_t)HW;
-    const uint32_t n0 = c.c_len, n1 = n0 + c.b_len, n2 = n1 + c.r_len;
+    f.fast = act && !e.over() && !c.leading() && c.c_len + c.nb() + c.nr() <= (uint32_t)HW;
+    const uint32_t n0 = c.c_len, n1 = n0 + c.nb(), n2 = n1 + c.nr();
     f.cand = f.fast && hl < n2;
     f.id = hl < n0 ? c.c_lo + hl : (hl < n1 ? c.b_lo + (hl - n0) : c.r_lo + (hl - n1));
-    const bool simple = (CS_DDZ_SIMPLE & 1) && simple_id(f.id, (uint32_t)tb.bomb_lo);
+    const bool simple = simple_id(f.id, (uint32_t)tb.bomb_lo);
     f.load = f.cand && !simple;
     f.cnt = f.cand && simple ? simple_cnt(f.id, (uint32_t)tb.bomb_lo) : ~0ull;
-    if (f.fast) ((uint32_t*)L.lst)[HW + hl] = 0u;   // the OR scratch: list entries 64..127
+    if (f.fast) ((uint32_t*)L.tst)[hl] = 0u;   // the OR scratch
     return f;
 }
-__device__ __forceinline__ void fast_finish(const Fast& f, uint64_t h, const Tab& tb, PairLds& L, uint32_t mis, int lane,
-                                            Legal& r)
+__device__ __forceinline__ void fast_finish(const Fast& f, uint64_t h, const Tab& tb, PairLds& L, int lane, Legal& r,
+                                            NzSink& z)
 {
     const uint32_t hl = (uint32_t)(lane & (HW - 1));
-    uint32_t* scr = (uint32_t*)L.lst + HW;
+    uint32_t* scr = (uint32_t*)L.tst;
     uint64_t cnt = f.cnt;
     // table loads only where a candidate is not simple (~5 % of these steps), waited for inside this branch: on gfx950
     // a load's wait also waits for every earlier store (vmcnt counts both), here the previous step's row stores
-    if constexpr ((CS_PROF_DDZ & 32) == 0) {   // profiling builds only: bit 5 drops the table loads of the legal build
-        if (__ballot(f.load)) cnt = f.load ? tb.cnt[f.id] : cnt;
-    }
+    if (__ballot(f.load)) cnt = f.load ? tb.cnt[f.id] : cnt;
     const bool pass = f.cand && contains(h, cnt);
     const uint32_t m = half32(__ballot(pass), lane);
     const uint32_t dw = f.id >> 5;
@@ -1005,30 +1042,30 @@ __device__ __forceinline__ void fast_finish(const Fast& f, uint64_t h, const Tab
     if (pass) atomicOr(scr + k, 1u << (f.id & 31u));
     wave_sync_lds();
     if (first) {
-        put_mask(L, dw, mis, scr[k]);
-        L.lst[k] = (uint16_t)dw;
+        L.val[k] = scr[k];
+        L.idx[k] = (uint16_t)dw;
+        atomicOr(&L.nzbm[dw >> 5], 1u << (dw & 31u));
     }
     if (f.fast) {
         r.total = (uint32_t)__popc(m);
-        r.nl = (uint32_t)__popc(fm);
+        z.n = (uint32_t)__popc(fm);
     }
 }
 
-// build_legal for each half's env (act: the half holds a live env that does not take the fast path); the mask image
-// must be zero on entry
-__device__ __forceinline__ Legal build_legal2(const Env& e, const Cand& c, const Tab& tb, const TabLds& T, PairLds& L,
-                                              uint32_t mis, int lane, bool act)
+// build_legal for each half's env (act: the half holds a live env on this path), in two parts: groups2 (pass a,
+// the group prefix counts in L.pre; returns whether the half has any playable group) and scan2 (passes b and c over
+// them; the sink takes every tested mask dword in ascending order)
+__device__ __forceinline__ bool groups2(const PEnv& e, const PCand& c, const Tab& tb, const TabLds& T, PairLds& L,
+                                        int lane, bool act)
 {
     const int hl = lane & (HW - 1);
-    Legal r;
-    r.total = 0;
-    r.nl = 0;
+    const bool own = act;   // only the halves on this path write their prefix counts (the other half's may be live)
     act = act && !e.over();
-    const uint64_t h = e.hand(e.cur);
+    const uint64_t h = e.hand(e.cur());
     // a. groups, 32 per pass and env; a pass whose groups no candidate range of either env meets only writes the
     // prefix counts (following a play: the same type's greater weights, the bombs, the rocket)
     uint32_t base = 0;
-#pragma unroll
+#pragma unroll 2
     for (int k = 0; k < MAX_GROUPS / HW; k++) {
         const int g = k * HW + hl;
         const bool may = act && c.meets((uint32_t)tb.kfirst[k], (uint32_t)tb.kfirst[k + 1]);
@@ -1039,22 +1076,32 @@ __device__ __forceinline__ Legal build_legal2(const Env& e, const Cand& c, const
                 pass = contains(h, (uint64_t)q.x | ((uint64_t)q.y << 32)) && c.ok(q.z & 0xFFFFu);
             }
             const uint32_t m = half32(__ballot(pass), lane);
-            if (g <= tb.ng) L.u.pre[g] = (uint16_t)(base + below32(m, hl));
+            if (own && g <= tb.ng) L.pre[g] = (uint16_t)(base + below32(m, hl));
             base += (uint32_t)__popc(m);
-        } else if (g <= tb.ng) {
-            L.u.pre[g] = (uint16_t)base;
+        } else if (own && g <= tb.ng) {
+            L.pre[g] = (uint16_t)base;
         }
     }
-    act = act && base != 0;
+    return act && base != 0;
+}
+template <class Sink>
+__device__ __forceinline__ Legal scan2(const PEnv& e, const PCand& c, const Tab& tb, const TabLds& T, PairLds& L,
+                                       int lane, bool act, Sink& sink)
+{
+    const int hl = lane & (HW - 1);
+    Legal r;
+    r.total = 0;
+    r.nl = 0;
     if (!__ballot(act)) return r;
+    const uint64_t h = e.hand(e.cur());
     wave_sync_lds();
-    // b. chunks of 32 dwords that any passing group reaches (lane k of a half: chunk k), their dwords listed in order;
-    // c. 4 listed dwords per env and batch
+    // b. chunks of 32 dwords that any passing group reaches (lane k of a half: chunk k), their dwords queued in order;
+    // c. 4 queued dwords per env and batch
     bool chp = false;
     if (act && hl < NCH) {
         const int last = hl * HW + HW - 1 < ND ? hl * HW + HW - 1 : ND - 1;
         const uint32_t lo = T.drange[hl * HW] & 0xFFFFu, hi = T.drange[last] >> 16;
-        chp = L.u.pre[hi + 1] > L.u.pre[lo];
+        chp = L.pre[hi + 1] > L.pre[lo];
     }
     uint32_t chunks = half32(__ballot(chp), lane);
     uint32_t tested = 0;
@@ -1066,105 +1113,79 @@ __device__ __forceinline__ Legal build_legal2(const Env& e, const Cand& c, const
         bool pass = false;
         if (has && d < ND) {
             const uint32_t dr = T.drange[d];
-            pass = L.u.pre[(dr >> 16) + 1] > L.u.pre[dr & 0xFFFFu];
+            pass = L.pre[(dr >> 16) + 1] > L.pre[dr & 0xFFFFu];
         }
         const uint32_t m = half32(__ballot(pass), lane);
-        if (pass) L.lst[(r.nl + below32(m, hl)) & (LIST_RING - 1)] = (uint16_t)d;
+        if (pass) L.tst[(r.nl + below32(m, hl)) & (TRING - 1)] = (uint16_t)d;
         r.nl += (uint32_t)__popc(m);
         while (__ballot(r.nl - tested >= 4u)) {
             const bool full = r.nl - tested >= 4u;
-            test_listed2(tested, full ? tested + 4u : tested, h, c, tb, L, mis, lane, r);
+            test_listed2(tested, full ? tested + 4u : tested, h, c, tb, L, lane, r, sink);
             tested += full ? 4u : 0u;
         }
     }
-    if (__ballot(tested < r.nl)) test_listed2(tested, r.nl, h, c, tb, L, mis, lane, r);
+    if (__ballot(tested < r.nl)) test_listed2(tested, r.nl, h, c, tb, L, lane, r, sink);
     return r;
 }
 
-// kth_legal's two-level scan over one env's whole mask image, all 64 lanes (k < the env's legal combos); the image's
-// bits are in id order, shifted by 8 mis bits: the result is the k-th set bit's position from byte 16, minus 8 mis
-__device__ __forceinline__ uint32_t kth_full(uint32_t k, const uint32_t* mask, int lane)
+// the k-th legal id of each half's env from its list (k < the env's legal count, n <= NZ_CAP entries): lane l of a half
+// holds entries l and 32 + l, a prefix scan of their popcounts finds the entry (the pass bit, merged into dword
+// ND - 1, is the largest id and never reached)
+__device__ __forceinline__ uint32_t kth_listed(uint32_t k, uint32_t n, const PairLds& L, int lane)
 {
-    uint32_t pc = 0;
-    if (lane < KTH_LANES) {
-        const uint4* w = (const uint4*)(mask + MASK_PAD) + lane * (KTH_WORDS / 4);
-#pragma unroll
-        for (int j = 0; j < KTH_WORDS / 4; j++) {
-            const uint4 x = w[j];
-            pc += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+    const uint32_t hl = (uint32_t)(lane & (HW - 1));
+    uint32_t v = hl < n ? L.val[hl] : 0u;
+    uint32_t pc = (uint32_t)__popc(v);
+    uint32_t inc = scan32(pc);
+    const uint32_t tot = hshfl(inc, lane, HW - 1);
+    uint32_t off = 0;
+    const bool hi = k >= tot;   // only with more than 32 entries
+    if (__ballot(hi)) {
+        const uint32_t v2 = hl + HW < n ? L.val[hl + HW] : 0u;
+        const uint32_t pc2 = (uint32_t)__popc(v2);
+        const uint32_t inc2 = scan32(pc2);
+        if (hi) {
+            v = v2;
+            pc = pc2;
+            inc = inc2;
+            k -= tot;
+            off = HW;
         }
     }
-    uint32_t inc = pc;
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
-        if (lane >= o) inc += y;
-    }
-    const int j = __builtin_ctzll(__ballot(inc > k));
-    k -= rl(inc, j) - rl(pc, j);
-    const uint32_t w = lane < KTH_WORDS ? mask[MASK_PAD + j * KTH_WORDS + lane] : 0u;
-    const uint32_t p2 = (uint32_t)__popc(w);
-    uint32_t inc2 = p2;
-#pragma unroll
-    for (int o = 1; o < KTH_WORDS; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)inc2, o);
-        if (lane >= o) inc2 += y;
-    }
-    const int q = __builtin_ctzll(__ballot(lane < KTH_WORDS && inc2 > k));
-    const uint32_t kk = k - (rl(inc2, q) - rl(p2, q));
-    return (uint32_t)(j * KTH_WORDS + q) * 32u + kth_bit(rl(w, q), kk, lane);
+    const uint32_t jm = half32(__ballot(inc > k), lane);
+    const uint32_t j = jm ? (uint32_t)__builtin_ctz(jm) : 0u;
+    const uint32_t incj = hshfl(inc, lane, j), pcj = hshfl(pc, lane, j), wj = hshfl(v, lane, j);
+    const uint32_t dj = L.idx[(off + j) & (NZ_CAP - 1)];
+    return dj * 32u + kth_bit32(wj, k - (incj - pcj), lane);
 }
 
-// kth_legal for each half's env: the listed dwords (at most 32: one per lane of the half), else the env's full scan
-__device__ __forceinline__ uint32_t kth_legal2(uint32_t k, const Legal& r, PairLds (&PL)[2], uint32_t mis, int lane)
+// mask dword d of the env's legal row from its list (0 when not listed)
+__device__ __forceinline__ uint32_t listed_dword(const PairLds& L, uint32_t d)
 {
-    const int hl = lane & (HW - 1), hf = lane >> 5;
-    const PairLds& L = PL[hf];
-    const bool pick = k < r.total;
-    const bool fast = pick && r.nl <= (uint32_t)HW, slow = pick && r.nl > (uint32_t)HW;
-    uint32_t res = (uint32_t)PASS;
-    if (__ballot(fast)) {
-        const bool in = fast && (uint32_t)hl < r.nl;
-        const uint32_t d = in ? L.lst[hl] : 0u;
-        const uint32_t w = in ? get_mask(L, d, mis) : 0u;
-        const uint32_t pc = (uint32_t)__popc(w);
-        const uint32_t inc = scan32(pc);
-        const uint32_t jm = half32(__ballot(inc > k), lane);
-        const uint32_t j = jm ? (uint32_t)__builtin_ctz(jm) : 0u;
-        const uint32_t incj = hshfl(inc, lane, j), pcj = hshfl(pc, lane, j), wj = hshfl(w, lane, j), dj = hshfl(d, lane, j);
-        const uint32_t kk = k - (incj - pcj);
-        const uint32_t bm = half32(__ballot(((wj >> hl) & 1u) && below32(wj, hl) == kk), lane);
-        if (fast) res = dj * 32u + (bm ? (uint32_t)__builtin_ctz(bm) : 0u);
-    }
-    const uint64_t sb = __ballot(slow);
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-        if ((sb >> (HW * j)) & 1u) {
-            const uint32_t id = kth_full(rl(k, HW * j), PL[j].mask, lane) - 8u * rl(mis, HW * j);
-            if (slow && hf == j) res = id;
-        }
-    }
-    return res;
+    const uint32_t wb = L.nzbm[d >> 5], b = d & 31u;
+    const uint32_t r = (uint32_t)L.npre[d >> 5] + (uint32_t)__popc(wb & ((1u << b) - 1u));
+    return ((wb >> b) & 1u) ? L.val[r & (NZ_CAP - 1)] : 0u;
 }
 
 // build_obs for each half's env, observed by `self` (per half)
-__device__ __forceinline__ void build_obs2(const Env& e, uint32_t self, PairLds& L, int lane)
+__device__ __forceinline__ void build_obs2(const PEnv& e, uint32_t self, PairLds& L, int lane)   // (L.q: played)
 {
     const int hl = lane & (HW - 1);
-    const uint32_t nt = e.ntrace;
-    const uint32_t h8 = e.hw4 & 0xFFFFu;
+    const uint32_t nt = e.ntrace();
     const uint32_t mate = 3u - self;
-    const uint64_t last_c = hshfl64(e.hcnt, lane, h8 == (uint32_t)PASS ? 10u : 11u);   // last non-pass action
+    // last non-pass action: the last trace entry unless it is a pass (or none: both give zero counts)
+    const uint64_t l11 = hshfl64(e.hcnt, lane, 11u), l10 = hshfl64(e.hcnt, lane, 10u);
+    const uint64_t last_c = l11 != 0ull ? l11 : l10;
     const uint64_t llv = hshfl64(e.hcnt, lane, 11u - (nt - 1u) % 3u);                 // landlord's last action
     const uint64_t ltv = hshfl64(e.hcnt, lane, 11u - (nt - 1u - mate) % 3u);          // teammate's last action
     const uint64_t ll_c = (self != 0u && nt >= 1u) ? llv : 0ull, lt_c = (self != 0u && nt > mate) ? ltv : 0ull;
     const int s = hl;
     const uint64_t u1 = e.hand(self == 0 ? 1u : 0u) + e.hand(self == 2 ? 1u : 2u);
-    const uint64_t u12 = self == 0 ? e.q2 : e.q0, u13 = self == 0 ? e.q1 : e.played(mate);
+    const uint64_t u12 = L.q[self == 0 ? 2 : 0], u13 = L.q[self == 0 ? 1 : mate];
     const uint64_t direct = keep64(s == 0, e.hand(self)) | keep64(s == 1, u1) | keep64(s == 2, last_c) |
                             keep64(s >= 3 && s <= 11, e.hcnt) | keep64(s == 12, u12) | keep64(s == 13, u13) |
                             keep64(s == 14, ll_c) | keep64(s == 15, lt_c);
-    if (s < NSEG) L.u.o.segv[s] = cards_bits(direct);
+    if (s < NSEG) L.segv[s] = cards_bits(direct);
     uint32_t p1, p2;
     if (self == 0) {
         const uint32_t n2 = num_cards(e.h2), n1 = num_cards(e.h1);
@@ -1178,13 +1199,15 @@ __device__ __forceinline__ void build_obs2(const Env& e, uint32_t self, PairLds&
     wave_sync_lds();
     const int x0 = hl == 0 ? 0 : 32 * hl - 16;
     const int sg = x0 / 54, off = x0 - 54 * sg;
-    const uint32_t v = (uint32_t)((L.u.o.segv[sg] >> off) | (L.u.o.segv[sg + 1] << (54 - off)));
+    const uint32_t v = (uint32_t)((L.segv[sg] >> off) | (L.segv[sg + 1] << (54 - off)));
     const uint32_t d1 = p1 - (uint32_t)x0, d2 = p2 - (uint32_t)x0;
-    L.u.o.bv[hl] = hl == 0 ? v << 16 : v | keep32(d1 < 32u, 1u << (d1 & 31u)) | keep32(d2 < 32u, 1u << (d2 & 31u));
+    L.bv[hl] = hl == 0 ? v << 16 : v | keep32(d1 < 32u, 1u << (d1 & 31u)) | keep32(d2 < 32u, 1u << (d2 & 31u));
 }
 
-// write_rows for each half's env
-__device__ __forceinline__ void write_rows2(const PairLds& L, uint8_t* orow, uint8_t* lrow, int lane)
+// the obs row and (lrow non-null) the legal row of each half's env, 16-B stores for the chunks inside a row and one
+// byte per lane for its two end chunks. The legal row's chunks are zero unless a listed dword falls into them (zw: the
+// half's nonzero bitmap words; a 32-chunk iteration j spans words 4 j - 1 .. 4 j + 4)
+__device__ __forceinline__ void write_rows2(const PairLds& L, uint8_t* orow, uint8_t* lrow, uint32_t zw, int lane)
 {
     const int hl = lane & (HW - 1);
     if (orow) {
@@ -1192,15 +1215,26 @@ __device__ __forceinline__ void write_rows2(const PairLds& L, uint8_t* orow, uin
 #pragma unroll
         for (int j = 0; j < 2; j++) {
             const int q = j * HW + hl;
-            if (q >= 1 && q < nchunks - 1) *(uint4*)(orow - mis + 16 * q) = obs_chunk(L.u.o.bv, q, mis);
+            if (q >= 1 && q < nchunks - 1) *(uint4*)(orow - mis + 16 * q) = obs_chunk(L.bv, q, mis);
         }
     }
-    if (lrow) {   // chunk q = image block q + 1 (the image is shifted by the row's misalignment)
+    if (lrow) {
         const int mis = (int)((uintptr_t)lrow & 15u), nchunks = (mis + LB + 15) >> 4;
-#pragma unroll CS_DDZ_LROW_UNROLL
-        for (int j = 0; j < (216 + HW - 1) / HW; j++) {
+#pragma unroll
+        for (int j = 0; j < LROW_IT; j++) {
             const int q = j * HW + hl;
-            if (q >= 1 && q < nchunks - 1) *(uint4*)(lrow - mis + 16 * q) = ((const uint4*)L.mask)[q + 1];
+            const bool touched = ((zw >> (j ? 4 * j - 1 : 0)) & 0x3Fu) != 0u;
+            if (q >= 1 && q < nchunks - 1) {
+                uint4 v = make_uint4(0u, 0u, 0u, 0u);
+                if (touched) {   // rare: gather the chunk's five mask dwords (row bytes 16 q - mis .. + 15)
+                    const uint32_t s = (uint32_t)(16 * q - mis), d = s >> 2, sh = s & 3u;
+                    const uint32_t w0 = listed_dword(L, d), w1 = listed_dword(L, d + 1), w2 = listed_dword(L, d + 2),
+                                   w3 = listed_dword(L, d + 3), w4 = listed_dword(L, d + 4);
+                    v = make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                                   __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+                }
+                *(uint4*)(lrow - mis + 16 * q) = v;
+            }
         }
     }
     // the rows' end chunks, a byte per lane: lanes 0..15 / 16..31 of a half the first / last chunk
@@ -1213,42 +1247,41 @@ __device__ __forceinline__ void write_rows2(const PairLds& L, uint8_t* orow, uin
             const int q = (hl & 16) ? nchunks - 1 : 0, o = 16 * q - mis + (hl & 15);
             if (o >= 0 && o < nbytes) {
                 const uint32_t x = 16u + (uint32_t)o;
-                row[o] = (uint8_t)(rr ? ((const uint8_t*)L.mask)[x + (uint32_t)mis] : (L.u.o.bv[x >> 5] >> (x & 31u)) & 1u);
+                row[o] = (uint8_t)(rr ? listed_dword(L, (uint32_t)o >> 2) >> (8 * (o & 3)) : (L.bv[x >> 5] >> (x & 31u)) & 1u);
             }
         }
     }
 }
 
-// the stream position of each half's env (WaveMt fields per lane)
-struct PairMt {
-    uint32_t pos, stale, dabs;
-    uint64_t key;
-};
-
-// deal a new game to half j's env with the whole wave (the one-env `deal`), then hand it to the half
+// deal a new game to half j's env with the whole wave (the one-env `deal`; its stream fields and the dealt deck in
+// that env's LDS), then hand it to the half
 template <bool PHX>
-__device__ __forceinline__ void deal_half(int j, Env& e, uint32_t& dlo, uint32_t& dhi, PairMt& pm, uint32_t* mt,
-                                          int64_t env_h, int lane)
+__device__ __forceinline__ void deal_half(int j, PEnv& e, PairLds& Lj, uint32_t* mt, int64_t env_h, int lane)
 {
-    const int src = HW * j;
     WaveMt<PHX> m;
-    const int64_t ej = (int64_t)rl((uint32_t)env_h, src) | ((int64_t)rl((uint32_t)((uint64_t)env_h >> 32), src) << 32);
+    const int64_t ej = (int64_t)rl((uint32_t)env_h, HW * j) | ((int64_t)rl((uint32_t)((uint64_t)env_h >> 32), HW * j) << 32);
     m.base = mt + ej * MT_WORDS;
-    m.pos = rl(pm.pos, src);
-    m.stale = rl(pm.stale, src);
-    m.dabs = rl(pm.dabs, src);
-    m.key = rl64(pm.key, src);
+    const uint32_t mp = Lj.mpos;
+    m.pos = mp & 0xFFFFu;
+    m.stale = mp >> 16;
+    m.dabs = Lj.mdabs;
+    m.key = Lj.mkey;
     Env es;
     deal(es, m, lane);
-    const uint32_t lo = (uint32_t)__shfl((int)es.deck, lane & (HW - 1)), hi = (uint32_t)__shfl((int)es.deck, HW + (lane & (HW - 1)));
-    if ((lane >> 5) == j) {
-        e = es;
-        dlo = lo;
-        dhi = (lane & (HW - 1)) < 54 - HW ? hi : 0u;
-        pm.pos = m.pos;
-        pm.stale = m.stale;
-        pm.dabs = m.dabs;
+    Lj.deck[lane] = (uint8_t)(lane < 54 ? es.deck : 0u);
+    if (lane < 3) Lj.q[lane] = 0ull;
+    if (lane == 0) {
+        Lj.mpos = m.pos | m.stale << 16;
+        Lj.mdabs = m.dabs;
     }
+    if ((lane >> 5) == j) {
+        e.h0 = es.h0; e.h1 = es.h1; e.h2 = es.h2;
+        e.hcnt = 0;
+        e.hid = NO_ACTION;
+        e.gw = 0;
+        e.sw = NONE << 16 | 0u << 20 | NONE << 24;   // ntrace 0, no greater player, landlord to play, not over
+    }
+    wave_sync_lds();
 }
 
 // k_rollout2's arguments, one struct: the kernel reads them from the kernarg segment through a pointer that every step
@@ -1275,7 +1308,8 @@ static_assert(offsetof(PairArgs, mt) == 0 && alignof(PairArgs) == 8 && sizeof(Pa
               "PairArgs: first kernarg at offset 0, 8-byte aligned");
 
 template <bool PHX>
-__global__ __launch_bounds__(PBLOCK, CS_DDZ_PAIR_MINW) void k_rollout2(PairArgs args)
+__global__ __launch_bounds__(PBLOCK) __attribute__((amdgpu_waves_per_eu(CS_DDZ_PAIR_MINW)))
+void k_rollout2(PairArgs args)
 {
     PairArgsK ak = (PairArgsK)__builtin_amdgcn_kernarg_segment_ptr();
     auto arg = [&]() -> const PairArgs& {
@@ -1289,127 +1323,131 @@ __global__ __launch_bounds__(PBLOCK, CS_DDZ_PAIR_MINW) void k_rollout2(PairArgs 
     const int T = args.T, kfl = args.kfl;
     __shared__ PairLds lds[PWPB][2];
     __shared__ TabLds tl;
-    const Tab& tb = arg().tb;
-    load_tab(tl, tb);                 // every thread of the block, before any wave leaves
+    load_tab(tl, args.tb);            // every thread of the block, before any wave leaves
     const int lane = (int)(threadIdx.x & (WAVE - 1)), hl = lane & (HW - 1), hf = lane >> 5;
     const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
-    const uint32_t bx = CS_DDZ_XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t bx = xcd_block(blockIdx.x, gridDim.x);   // rows shared by neighbouring blocks meet in one L2
     const int64_t env = (int64_t)bx * (2 * PWPB) + 2 * wid + hf;
     const bool valid = env < n;
     if (!__ballot(valid)) return;
-    PairLds (&PL)[2] = lds[wid];
-    PairLds& L = PL[hf];
-    // the env's state words (lanes 0..31 of its half: words 0..31, lanes 0..3: 32..35) and stream position
-    const uint32_t* srow = st + (valid ? env : 0) * WORDS;
-    const uint32_t wlo = valid ? srow[hl] : 0u, whi = valid && hl < WORDS - HW ? srow[HW + hl] : 0u;
-    auto F = [&](uint32_t w) { return hshfl(wlo, lane, w); };
-    Env e;
-    e.h0 = (uint64_t)F(0) | ((uint64_t)F(1) << 32);
-    e.h1 = (uint64_t)F(2) | ((uint64_t)F(3) << 32);
-    e.h2 = (uint64_t)F(4) | ((uint64_t)F(5) << 32);
-    e.q0 = (uint64_t)F(6) | ((uint64_t)F(7) << 32);
-    e.q1 = (uint64_t)F(8) | ((uint64_t)F(9) << 32);
-    e.q2 = (uint64_t)F(10) | ((uint64_t)F(11) << 32);
-    e.hw0 = F(W_HIST);
-    e.hw1 = F(W_HIST + 1);
-    e.hw2 = F(W_HIST + 2);
-    e.hw3 = F(W_HIST + 3);
-    const uint32_t w16 = F(W_HIST + 4);
-    e.hw4 = w16 | (NO_ACTION << 16);
-    e.ggrp = w16 >> 16;
-    {
-        const uint32_t id = hl >= 3 && hl <= 11 ? e.hist((uint32_t)(hl - 3)) : NO_ACTION;
-        e.hcnt = id < (uint32_t)PASS ? tb.cnt[id] : 0ull;
-    }
-    e.ntrace = F(W_NTRACE);
-    {
+    PairLds& L = lds[wid][hf];
+    PEnv e;
+    {   // the env's state words (lanes 0..31 of its half: words 0..31, the deck bytes) and stream position
+        const uint32_t* srow = st + (valid ? env : 0) * WORDS;
+        const uint32_t wlo = valid ? srow[hl] : 0u;
+        auto F = [&](uint32_t w) { return hshfl(wlo, lane, w); };
+        e.h0 = (uint64_t)F(0) | ((uint64_t)F(1) << 32);
+        e.h1 = (uint64_t)F(2) | ((uint64_t)F(3) << 32);
+        e.h2 = (uint64_t)F(4) | ((uint64_t)F(5) << 32);
+        const uint64_t qv = (uint64_t)F(6 + 2 * (hl % 3)) | ((uint64_t)F(7 + 2 * (hl % 3)) << 32);
+        if (hl < 3) L.q[hl] = qv;
+        const uint32_t k = (uint32_t)(hl >= 3 ? hl - 3 : 0);   // lanes 3..11: trace entry hl - 3 of the last 9
+        const uint32_t hw = F(W_HIST + (k >> 1));
+        e.hid = hl >= 3 && hl <= 11 ? (hw >> (16 * (k & 1))) & 0xFFFFu : NO_ACTION;
+        e.hcnt = e.hid < (uint32_t)PASS ? args.tb.cnt[e.hid] : 0ull;
         const uint32_t g = F(W_GREATER), c = F(W_CUR);
-        e.greater = g & 0xFFFFu;
-        e.gplay = g >> 16;
-        e.cur = c & 0xFFu;
-        e.winner = valid ? (c >> 8) & 0xFFu : 0u;   // a missing env stays "over" and is never dealt
-    }
-    (void)whi;
-    e.deck = 0;
-    const uint8_t* dk = (const uint8_t*)(srow + W_DECK);
-    uint32_t dlo = valid ? dk[hl] : 0u, dhi = valid && hl < 54 - HW ? dk[HW + hl] : 0u;
-    PairMt pm;
-    {
-        const uint32_t w = valid ? ctl[env] : 0u;
-        pm.pos = w & 0x7FFu;
-        pm.stale = (w >> 16) & 1u;
-        pm.dabs = 0;
-        pm.key = 0;
-        if constexpr (PHX) {
-            const uint32_t* b = mt + (valid ? env : 0) * MT_WORDS;
-            pm.key = valid ? (uint64_t)b[0] | (uint64_t)b[1] << 32 : 0ull;
-            pm.dabs = valid ? b[2] : 0u;
+        e.gw = (g >> 16) | (F(W_HIST + 4) & 0xFFFF0000u);
+        const uint32_t winner = valid ? (c >> 8) & 0xFFu : 0u;   // a missing env stays "over" and is never dealt
+        e.sw = F(W_NTRACE) | (g & 3u) << 16 | (c & 3u) << 20 | winner << 24;
+        const uint8_t* dk = (const uint8_t*)(srow + W_DECK);
+        L.deck[hl] = valid ? dk[hl] : 0u;
+        L.deck[HW + hl] = valid && hl < 54 - HW ? dk[HW + hl] : 0u;
+        if (hl == 0) {
+            L.mpos = valid ? ctl[env] & 0x1FFFFu : 0u;   // position | stale << 16
+            L.mdabs = 0;
+            L.mkey = 0;
+            if constexpr (PHX) {
+                const uint32_t* b = mt + (valid ? env : 0) * MT_WORDS;
+                L.mkey = valid ? (uint64_t)b[0] | (uint64_t)b[1] << 32 : 0ull;
+                L.mdabs = valid ? b[2] : 0u;
+            }
         }
+        wave_sync_lds();
     }
     {
         const uint64_t need = __ballot(valid && e.over());
-#pragma unroll
+#pragma unroll 1
         for (int j = 0; j < 2; j++)
-            if ((need >> (HW * j)) & 1u) deal_half<PHX>(j, e, dlo, dhi, pm, mt, env, lane);
+            if ((need >> (HW * j)) & 1u) deal_half<PHX>(j, e, lds[wid][j], mt, env, lane);
     }
-    const uint64_t genv = args.env_base + (uint64_t)env;
     uint32_t rr_lane = 0;
-    bool dirty = true;   // CS_DDZ_CLEAN: the half's image holds bits the previous step did not clean
     for (int t = 0; t < T; t++) {
+        // the lane id made opaque at each step: lane-derived values (LDS and row offsets) are recomputed where they are
+        // used instead of hoisted out of the loop -- held, they were spilled, and a spill reload waits on vmcnt, i.e.
+        // on every row store the wave has in flight
+        int lane_o = lane;
+        asm volatile("" : "+v"(lane_o));
+        const int lane = lane_o, hl = lane & (HW - 1);
         const PairArgs& A = arg();
         const Tab& tb = A.tb;
         const cs_traj_out& out = A.out;
-        const uint64_t seed = A.seed, t0 = A.t0;
         const int64_t row = (int64_t)t * n + env;
-        if (CS_DDZ_CLEAN == 0 || __ballot(dirty)) {   // zero the mask image of both envs: 224 uint4 each, 32 lanes per env
-            uint4* z = (uint4*)L.mask;
-#pragma unroll
-            for (int j = 0; j < (PMASK_WORDS / 4 + HW - 1) / HW; j++) {
-                const int q = j * HW + hl;
-                if ((CS_DDZ_PAD || q < PMASK_WORDS / 4) && (CS_DDZ_CLEAN == 0 || dirty)) z[q] = make_uint4(0, 0, 0, 0);
+        uint8_t* const lrow = (uint8_t*)out.legal + row * LB;
+        wave_sync_lds();                  // the previous step's row writer has read the list
+        if (hl < NZBM) L.nzbm[hl] = 0u;
+        wave_sync_lds();
+        const PCand cd = pcand(e, tb, tl);
+        const Fast fst = fast_issue(e, cd, tb, L, lane, valid && (kfl & 1) == 0);   // kernel flag bit 0: off
+        NzSink z{&L, 0u};
+        const bool gact = groups2(e, cd, tb, tl, L, lane, valid && !fst.fast);
+        Legal lg = scan2(e, cd, tb, tl, L, lane, gact, z);
+        build_obs2(e, e.cur(), L, lane);
+        if (__ballot(fst.fast)) fast_finish(fst, e.hand(e.cur()), tb, L, lane, lg, z);
+        wave_sync_lds();
+        // the pass bit (following a play): OR-ed into the list's last dword when that is dword ND - 1, else appended
+        const bool pass = valid && !e.over() && !cd.leading();
+        if (__ballot(pass)) {
+            const uint32_t lastd = z.n > 0u && z.n <= (uint32_t)NZ_CAP ? L.idx[z.n - 1u] : 0xFFFFu;
+            const bool merge = lastd == (uint32_t)(ND - 1);
+            if (pass && hl == 0) {
+                if (merge) L.val[z.n - 1u] |= 1u << (PASS & 31);
+                else if (z.n < (uint32_t)NZ_CAP) {
+                    L.val[z.n] = 1u << (PASS & 31);
+                    L.idx[z.n] = (uint16_t)(ND - 1);
+                    atomicOr(&L.nzbm[(ND - 1) >> 5], 1u << ((ND - 1) & 31));
+                }
             }
+            z.n += pass && !merge ? 1u : 0u;
         }
+        const bool ovf = valid && (z.n > (uint32_t)NZ_CAP || (kfl & 2) != 0);   // kernel flag bit 1: every step
         wave_sync_lds();
-        const uint32_t lmis = (uint32_t)(((uintptr_t)out.legal + (uint64_t)row * CS_DDZ_ROWSTRIDE_L) & 15u);   // the image's shift
-        const Cand cd = cand_of(e, tb, tl);
-        const Fast fst = fast_issue(e, cd, tb, L, lane, valid && (kfl & 1) == 0);   // kernel flag bit 0: A/B only
-        Legal lg = build_legal2(e, cd, tb, tl, L, lmis, lane, valid && !fst.fast);
-        if (!(CS_PROF_DDZ & 16)) build_obs2(e, e.cur, L, lane);   // profiling builds only: bit 4 skips the obs image
-        if (__ballot(fst.fast)) fast_finish(fst, e.hand(e.cur), tb, L, lmis, lane, lg);
-        wave_sync_lds();
-        const uint32_t count = lg.total + (cd.leading ? 0u : 1u);
-        if ((t & (HW - 1)) == 0) rr_lane = philox_u32(seed, genv, t0 + (uint64_t)(t + hl));
+        // the bitmap's prefix ranks and nonzero words
+        const uint32_t bw = hl < NZBM ? L.nzbm[hl] : 0u;
+        const uint32_t bpc = (uint32_t)__popc(bw);
+        if (hl < NZBM) L.npre[hl] = (uint8_t)(scan32(bpc) - bpc);
+        const uint32_t zw = half32(__ballot(bw != 0u), lane);
+        // the policy pick: the k-th legal id, k uniform from Philox (pass = the last when following)
+        const uint32_t count = lg.total + (cd.leading() ? 0u : 1u);
+        if ((t & (HW - 1)) == 0) rr_lane = philox_u32(A.seed, A.env_base + (uint64_t)env, A.t0 + (uint64_t)(t + hl));
         const uint32_t rr = hshfl(rr_lane, lane, (uint32_t)(t & (HW - 1)));
-        const uint32_t a = kth_legal2((uint32_t)(((uint64_t)rr * count) >> 32), lg, PL, lmis, lane);
+        const uint32_t k = (uint32_t)(((uint64_t)rr * count) >> 32);
+        uint32_t a = (uint32_t)PASS;
+        if (__ballot(k < lg.total && !ovf)) {
+            const uint32_t ka = kth_listed(k, z.n, L, lane);
+            if (k < lg.total && !ovf) a = ka;
+        }
+        if (__ballot(ovf)) {   // the overflow path: the legal scan again, the row straight to HBM
+            RowCursor rc{ovf ? lrow : nullptr, 0u, k, 0u, (uint32_t)PASS, pass};
+            if (__ballot(ovf && !gact)) groups2(e, cd, tb, tl, L, lane, ovf && !gact);   // kernel flag 2 on fast steps
+            scan2(e, cd, tb, tl, L, lane, ovf, rc);
+            rc.finish(lane);
+            if (ovf && k < lg.total) a = rc.found;
+        }
         // the action's table entries, loaded now so that their latency hides behind the row writes
         const bool play = valid && a != (uint32_t)PASS;
-        const bool sa = (CS_DDZ_SIMPLE & 2) && simple_id(a, (uint32_t)tb.bomb_lo);
-        const uint64_t ca = play ? (sa ? simple_cnt(a, (uint32_t)tb.bomb_lo) : tb.cnt[a]) : 0ull;
-        const uint32_t ga = play ? (sa ? simple_gid(a, (uint32_t)tb.bomb_lo, (uint32_t)tb.bomb_g) : (uint32_t)tb.gid[a]) : 0u;
-        if (valid && !cd.leading && hl == 0) ((uint8_t*)L.mask)[16u + lmis + PASS / 8] |= (uint8_t)(1u << (PASS & 7));
+        const uint64_t ca = play ? tb.cnt[a] : 0ull;
+        const uint32_t ga = play ? (uint32_t)tb.gid[a] : 0u;
         wave_sync_lds();
-        write_rows2(L, valid && !(CS_PROF_DDZ & 2) ? (uint8_t*)out.obs + row * CS_DDZ_ROWSTRIDE_O : nullptr,
-                    valid && !(CS_PROF_DDZ & 1) ? (uint8_t*)out.legal + row * CS_DDZ_ROWSTRIDE_L : nullptr, lane);
-        if constexpr (CS_DDZ_CLEAN != 0) {
-            // clean after the row is out: zero the dwords this step wrote (all listed unless the list ring wrapped)
-            // and the pass byte, instead of the whole image at the next step
-            dirty = lg.nl > (uint32_t)LIST_RING || (kfl & 2) != 0;   // kernel flag bit 1: A/B only
-            wave_sync_lds();
-#pragma unroll
-            for (int j = 0; j < LIST_RING / HW; j++) {
-                const uint32_t k = (uint32_t)(j * HW + hl);
-                if (!dirty && k < lg.nl) put_mask(L, L.lst[k], lmis, 0u);
-            }
-            if (hl == 0) ((uint8_t*)L.mask)[16u + lmis + PASS / 8] = 0;
-        }
-        const uint32_t p = e.cur;
-        if (valid) e.apply_with(a, ca, ga, hl);
+        write_rows2(L, valid && !(CS_PROF_DDZ & 2) ? (uint8_t*)out.obs + row * OBS : nullptr,
+                    valid && !ovf && !(CS_PROF_DDZ & 1) ? lrow : nullptr, zw, lane);
+        const uint32_t p = e.cur();
+        if (valid) e.apply_with(a, ca, ga, hl, L.q);
         const bool done = valid && e.over();
         if (valid && hl == 0) {
             ((uint8_t*)out.player)[row] = (uint8_t)p;
             ((int16_t*)out.action)[row] = (int16_t)a;
             float r[3] = {0.f, 0.f, 0.f};
-            if (done) payoffs(e, r);
+            if (done) payoffs(e.winner(), r);
             float* o = (float*)out.reward + row * P;
             o[0] = r[0]; o[1] = r[1]; o[2] = r[2];
             ((uint8_t*)out.done)[row] = (uint8_t)done;
@@ -1421,29 +1459,34 @@ __global__ __launch_bounds__(PBLOCK, CS_DDZ_PAIR_MINW) void k_rollout2(PairArgs 
                     wave_sync_lds();
                     build_obs2(e, q, L, lane);
                     wave_sync_lds();
-                    write_rows2(L, done ? (uint8_t*)out.final_obs + (row * P + q) * OBS : nullptr, nullptr, lane);
+                    write_rows2(L, done ? (uint8_t*)out.final_obs + (row * P + q) * OBS : nullptr, nullptr, 0u, lane);
                 }
             }
-#pragma unroll
+#pragma unroll 1
             for (int j = 0; j < 2; j++)
-                if ((fin >> (HW * j)) & 1u) deal_half<PHX>(j, e, dlo, dhi, pm, mt, env, lane);
+                if ((fin >> (HW * j)) & 1u) deal_half<PHX>(j, e, lds[wid][j], mt, env, lane);
         }
     }
+    // the state back: words 0..19 (lanes 0..4 of the half, 16 B each), the deck bytes, the stream position
+    const uint32_t h01 = hshfl(e.hid, lane, 3u + 2u * (uint32_t)(hl - 3)) | hshfl(e.hid, lane, 4u + 2u * (uint32_t)(hl - 3)) << 16;
+    const uint32_t hw0 = hshfl(h01, lane, 3u), hw1 = hshfl(h01, lane, 4u), hw2 = hshfl(h01, lane, 5u),
+                   hw3 = hshfl(h01, lane, 6u), hw4 = hshfl(h01, lane, 7u);
     if (valid) {
         if (hl == 0) {
             uint4* o = (uint4*)(st + env * WORDS);
             o[0] = make_uint4((uint32_t)e.h0, (uint32_t)(e.h0 >> 32), (uint32_t)e.h1, (uint32_t)(e.h1 >> 32));
-            o[1] = make_uint4((uint32_t)e.h2, (uint32_t)(e.h2 >> 32), (uint32_t)e.q0, (uint32_t)(e.q0 >> 32));
-            o[2] = make_uint4((uint32_t)e.q1, (uint32_t)(e.q1 >> 32), (uint32_t)e.q2, (uint32_t)(e.q2 >> 32));
-            o[3] = make_uint4(e.hw0, e.hw1, e.hw2, e.hw3);
-            o[4] = make_uint4((e.hw4 & 0xFFFFu) | (e.ggrp << 16), e.ntrace, e.greater | (e.gplay << 16),
-                              e.cur | (e.winner << 8));
-            ctl[env] = pm.pos | (pm.stale << 16) | (PHX ? CTL_PHX : 0u);
-            if constexpr (PHX) mt[env * MT_WORDS + 2] = pm.dabs;
+            const uint64_t q0 = L.q[0], q1 = L.q[1], q2 = L.q[2];
+            o[1] = make_uint4((uint32_t)e.h2, (uint32_t)(e.h2 >> 32), (uint32_t)q0, (uint32_t)(q0 >> 32));
+            o[2] = make_uint4((uint32_t)q1, (uint32_t)(q1 >> 32), (uint32_t)q2, (uint32_t)(q2 >> 32));
+            o[3] = make_uint4(hw0, hw1, hw2, hw3);
+            o[4] = make_uint4((hw4 & 0xFFFFu) | (e.gw & 0xFFFF0000u), e.ntrace(),
+                              e.greater() | (e.gw & 0xFFFFu) << 16, e.cur() | e.winner() << 8);
+            ctl[env] = L.mpos | (PHX ? CTL_PHX : 0u);
+            if constexpr (PHX) mt[env * MT_WORDS + 2] = L.mdabs;
         }
         uint8_t* db = (uint8_t*)(st + env * WORDS + W_DECK);
-        db[hl] = (uint8_t)dlo;
-        db[HW + hl] = (uint8_t)dhi;
+        db[hl] = L.deck[hl];
+        db[HW + hl] = L.deck[HW + hl];
     }
 }
 
@@ -1536,19 +1579,10 @@ hipError_t launch_observe(const Buffers& b, int32_t p, const cs_step_out& o, hip
 hipError_t launch_rollout(const Buffers& b, int32_t T, uint64_t seed, uint64_t t0, uint64_t env_base,
                           const cs_traj_out& o, hipStream_t s)
 {
-    if constexpr (CS_DDZ_PAIR) {
-        const dim3 g((unsigned)((b.n + 2 * PWPB - 1) / (2 * PWPB)));
-        const PairArgs a{b.mt, b.ctl, b.state, b.n, seed, t0, env_base, o, *(const Tab*)b.table, T, b.serial_refill};
-        if (b.rng_mode == CS_RNG_PHILOX) hipLaunchKernelGGL(k_rollout2<true>, g, dim3(PBLOCK), 0, s, a);
-        else hipLaunchKernelGGL(k_rollout2<false>, g, dim3(PBLOCK), 0, s, a);
-        return hipGetLastError();
-    }
-    if (b.rng_mode == CS_RNG_PHILOX)
-        hipLaunchKernelGGL(k_rollout<true>, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0, env_base, o,
-                           *(const Tab*)b.table);
-    else
-        hipLaunchKernelGGL(k_rollout<false>, grid_of(b.n), dim3(BLOCK), 0, s, b.mt, b.ctl, b.state, b.n, T, seed, t0, env_base, o,
-                           *(const Tab*)b.table);
+    const dim3 g((unsigned)((b.n + 2 * PWPB - 1) / (2 * PWPB)));
+    const PairArgs a{b.mt, b.ctl, b.state, b.n, seed, t0, env_base, o, *(const Tab*)b.table, T, b.serial_refill};
+    if (b.rng_mode == CS_RNG_PHILOX) hipLaunchKernelGGL(k_rollout2<true>, g, dim3(PBLOCK), 0, s, a);
+    else hipLaunchKernelGGL(k_rollout2<false>, g, dim3(PBLOCK), 0, s, a);
     return hipGetLastError();
 }
 

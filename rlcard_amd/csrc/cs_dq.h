@@ -1,5 +1,5 @@
 // cs_dq.h -- the deal queue of the lane-per-env games whose deal depends only on the env's stream (heads-up hold'em,
-// cs_limit.h; Leduc, cs_leduc.h): deals drawn ahead, in stream order, popped by the game resets. Shared by the rollout
+// cs_limit.h, cs_nolimit.h): deals drawn ahead, in stream order, popped by the game resets. Shared by the rollout
 // skeleton (cs_skeleton.h) and the CFR kernel (cs_cfr.hip), which resets through the same queue.
 #pragma once
 #include <type_traits>
@@ -11,39 +11,20 @@ namespace cs {
 template <class G, class = void>
 struct DqOf {
     static constexpr int value = 0, words = 0, cb = 0, xb = 0;
-    static constexpr bool regs = false, hbm = false;
 };
 template <class G>
 struct DqOf<G, std::void_t<decltype(G::DQ)>> {
     static constexpr int value = G::DQ, words = G::DQ > 0 ? 1 + 2 * G::DQ : 0;
     // header fields (cs_limit.h): count bits, then head bits (cb - 1), from bit xb the dealer bits and draws[8:7]
     static constexpr int cb = G::DQ == 8 ? 4 : G::DQ == 4 ? 3 : 2, xb = 2 * cb - 1;
-    static constexpr bool regs = G::DQ_REGS, hbm = G::DQ_HBM;
 };
 
-// queue word views: DqMem = words `stride` apart (state in HBM: n; LDS copy: 1), DqRegs = the words in registers
-// (dynamic slots through select chains, so the array never goes to scratch)
+// the queue words of one env, `stride` apart (state in HBM: n; the rollout's LDS copy: 1)
 struct DqMem {
     uint32_t* p;
     int64_t stride;
     __device__ __forceinline__ uint32_t get(uint32_t i) const { return p[i * stride]; }
     __device__ __forceinline__ void set(uint32_t i, uint32_t v) { p[i * stride] = v; }
-};
-template <int NW>
-struct DqRegs {
-    uint32_t w[NW];
-    __device__ __forceinline__ uint32_t get(uint32_t i) const
-    {
-        uint32_t r = w[0];
-#pragma unroll
-        for (int k = 1; k < NW; k++) r = i == (uint32_t)k ? w[k] : r;
-        return r;
-    }
-    __device__ __forceinline__ void set(uint32_t i, uint32_t v)
-    {
-#pragma unroll
-        for (int k = 0; k < NW; k++) w[k] = i == (uint32_t)k ? v : w[k];
-    }
 };
 
 // draw the env's next deal into its queue (the caller checks for room)

@@ -8,10 +8,8 @@ namespace cs {
 
 // Byte-ring slots of the lane-per-env games' MT19937 streams (cs_ring.h): 16 = 15 blocks twisted per refill from one
 // read and one write of the block words (8: seven, 4: three)
-#ifndef CS_RING_SLOTS
-#define CS_RING_SLOTS 16
-#endif
-constexpr int RING_ENV_WORDS_HOST = 624 + CS_RING_SLOTS * 624 / 4;   // u32 per env: block words + the ring bytes
+constexpr int RING_SLOTS_HOST = 16;
+constexpr int RING_ENV_WORDS_HOST = 624 + RING_SLOTS_HOST * 624 / 4;   // u32 per env: block words + the ring bytes
 
 // cs_set_step_record: the single-step kernels also write env `env`'s packed state words to `words`, then -- after a
 // system-scope fence that orders every output store of that env's wave -- `seqv` to *seq (both typically in mapped

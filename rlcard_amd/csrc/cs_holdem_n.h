@@ -123,16 +123,12 @@ __device__ __forceinline__ void holdem_judge(const uint32_t (&value)[P], const i
     }
 }
 
-#ifndef CS_DEALK_SWAR
-#define CS_DEALK_SWAR 1   // 0: the JV table below (A/B)
-#endif
 // The deal of a P-player hold'em game (limitholdem/dealer.py: shuffle 52, deal_card = pop): the K = 2P + 5 dealt
-// positions 51 .. 51 - K + 1 are fixed by the first K Fisher-Yates swaps, tracked in registers as in holdem_deal2
-// (JV[k] = j | card moved to j << 8); the other 51 - K draws only consume the stream. d[k] = card dealt k-th.
+// positions 51 .. 51 - K + 1 are fixed by the first K Fisher-Yates swaps, tracked in registers as in holdem_deal2;
+// the other 51 - K draws only consume the stream. d[k] = card dealt k-th.
 template <int K, class Rng>
 __device__ __forceinline__ void holdem_deal_k(Rng& rng, uint32_t (&d)[K])
 {
-#if CS_DEALK_SWAR
     // the K draws first (stream order), then every dealt position 51 - k traced back through the swaps q = K-1 .. 0
     // four per word (SWAR byte compares, as holdem_deal2): ~K^2/4 word steps instead of the K^2/2 pairwise lookups
     constexpr int NW = (K + 3) / 4;
@@ -162,23 +158,6 @@ __device__ __forceinline__ void holdem_deal_k(Rng& rng, uint32_t (&d)[K])
     }
 #pragma unroll
     for (int k = 0; k < K; k++) d[k] = (X[k >> 2] >> (8 * (k & 3))) & 63u;
-    rng.skip_intervals(51u - K);
-    return;
-#endif
-    uint32_t JV[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        const uint32_t i = 51 - k, j = rng.interval(i);
-        uint32_t vi = i, vj = j;
-#pragma unroll
-        for (int q = 0; q < k; q++) {   // oldest -> newest: the newest write to a position wins
-            const uint32_t jq = JV[q] & 255u, vq = JV[q] >> 8;
-            vi = jq == i ? vq : vi;
-            vj = jq == j ? vq : vj;
-        }
-        JV[k] = j | (vi << 8);
-        d[k] = vj;
-    }
     rng.skip_intervals(51u - K);
 }
 

@@ -15,62 +15,24 @@
 #pragma once
 #include "cs_device.h"
 
-#ifndef CS_LEDUC_STAGE_RF
-#define CS_LEDUC_STAGE_RF 24   // measured 1.94-1.99 -> 1.90-1.91 ms (40: 1.91-1.92, 56: 1.93-1.95)
-#endif
-#ifndef CS_LEDUC_RESTAGE_B
-#define CS_LEDUC_RESTAGE_B 4
-#endif
-#ifndef CS_LEDUC_REFILL_K
-#define CS_LEDUC_REFILL_K 1
-#endif
-#ifndef CS_LEDUC_RESET_SCAN
-#define CS_LEDUC_RESET_SCAN 1
-#endif
-#ifndef CS_LEDUC_RESET_SWAR
-#define CS_LEDUC_RESET_SWAR 1
-#endif
-#ifndef CS_LEDUC_MIN_WAVES
-#define CS_LEDUC_MIN_WAVES 6
-#endif
-#ifndef CS_LEDUC_SPARSE_OBS
-#define CS_LEDUC_SPARSE_OBS 1   // rollout obs rows through row_write_sparse (0: the expanded bitmap, RowWriter)
-#endif
-#ifndef CS_LEDUC_STAGE_W
-#define CS_LEDUC_STAGE_W 64
-#endif
-#ifndef CS_LEDUC_DQ
-#define CS_LEDUC_DQ 0   // deals drawn ahead per env (cs_dq.h; 0 = none): a reset pops one, a lockstep pass refills
-#endif
-#ifndef CS_LEDUC_STAGE_R
-
-#define CS_LEDUC_STAGE_R 12
-#endif
+#include "cs_prof.h"
 
 namespace cs {
 
 struct Leduc {
-    static_assert(CS_LEDUC_DQ == 0 || CS_LEDUC_DQ == 2 || CS_LEDUC_DQ == 4, "Leduc deal queue: 0, 2 or 4 deals");
-    static constexpr int GW = 2;   // game words; the deal queue (CS_LEDUC_DQ > 0) follows
-    static constexpr int DQ = CS_LEDUC_DQ;
-    static constexpr bool DQ_REGS = true, DQ_HBM = false;   // rollout: the queue words in registers
-    static constexpr int OBS = 36, A = 4, P = 2, LB = 1, WORDS = GW + (DQ > 0 ? 1 + 2 * DQ : 0), ACTION_BYTES = 1;
+    // (no deal queue: drawing deals ahead, as Limit / No-limit do, measured slower here -- profiles/EXPERIMENTS.md)
+    static constexpr int OBS = 36, A = 4, P = 2, LB = 1, WORDS = 2, ACTION_BYTES = 1;
     static constexpr int NB = 2;  // obs bitmap words
     static constexpr bool RING = true;          // MT stream as the byte ring (cs_ring.h)
     static constexpr bool RAW_OBS = false;
     static constexpr int SCRATCH_WORDS = 0;
     // MT staging (see MtLaneT)
-    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = CS_LEDUC_STAGE_W, STAGE_PAD = 4, STAGE_R = CS_LEDUC_STAGE_R;
-    static constexpr int STAGE_RF = CS_LEDUC_STAGE_RF;    // batch restage threshold (ring_restage_wave)
-    static constexpr int RESTAGE_B = CS_LEDUC_RESTAGE_B;  // lanes restaged per pass (loads in flight): 4 > 8 > 1
-    static constexpr int MIN_WAVES = CS_LEDUC_MIN_WAVES;  // rollout waves per SIMD the register budget must allow
+    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 64, STAGE_PAD = 4, STAGE_R = 12;
+    static constexpr int STAGE_RF = 24;   // batch restage threshold (ring_restage_wave): 24 > 40 > 56
+    static constexpr int RESTAGE_B = 4;   // lanes restaged per pass (loads in flight): 4 > 8 > 1
+    static constexpr int MIN_WAVES = 6;   // rollout waves per SIMD the register budget must allow
     static constexpr int EPW = 64;        // rollout envs per wave (lane_ctx)
-    // k_rollout (cs_skeleton.h): rows stored where they are produced, 8-B reward rows. Stores-last + reward pairs
-    // (round 5) were 4.1 vs 5.1 ms on physically contiguous trajectories but 6-7 % slower on every torch allocation
-    // once the stores-first step compiled as well as round 4's (4.22 vs 4.51 ms, same box, same allocations)
-    static constexpr bool STORES_LAST = false;
-    static constexpr bool REWARD_PAIRS = false;
-    static constexpr int REFILL_K = CS_LEDUC_REFILL_K;    // 1: refills are rare here, and K = 2 costs 12 VGPRs = 1 wave/SIMD
+    static constexpr int REFILL_K = 1;    // refills are rare here, and K = 2 costs 12 VGPRs = 1 wave/SIMD
     __device__ __forceinline__ void bind(uint32_t*, const GameParams&) {}
     enum { CALL = 0, RAISE = 1, FOLD = 2, CHECK = 3 };
 
@@ -116,7 +78,7 @@ struct Leduc {
 
     // the same row as the byte positions of its ones (row_write_sparse): hand rank, public rank + 3 (absent: the hand
     // position again), my chips + 6, the others' chips + 21
-    static constexpr int SPARSE_K = CS_LEDUC_SPARSE_OBS ? 4 : 0;
+    static constexpr int SPARSE_K = 4;
     __device__ __forceinline__ uint32_t observe_pos(int player, uint32_t (&pos)[4]) const
     {
         const int my = player ? in1 : in0, hand = (player ? h1 : h0) >> 1;
@@ -186,11 +148,11 @@ struct Leduc {
     template <class Rng>
     __device__ __forceinline__ static uint32_t draw_deal(Rng& rng)
     {
-#ifdef CS_PROF_NO_RESET   // profiling builds only: wrong deals, timing of the reset
+#if CS_PROF_NO_RESET   // profiling builds only (cs_prof.h)
         rng.advance_by(7u);
         return 0u | 2u << 3 | 4u << 6 | (rng.pos & 1u) << 9;
 #endif
-        if constexpr (Rng::kMode == STAGE_LDS && CS_LEDUC_RESET_SWAR) {
+        if constexpr (Rng::kMode == STAGE_LDS) {
             uint32_t code;
             if (deal_swar(rng, code)) return code;
         }
@@ -209,7 +171,7 @@ struct Leduc {
                 q++;
             }
         };
-        if constexpr (Rng::kMode == STAGE_LDS && CS_LEDUC_RESET_SCAN) {
+        if constexpr (Rng::kMode == STAGE_LDS) {
             const uint32_t k0 = rng.staged_offset();
             uint32_t k = k0;
             while (q < 6 && k < rng.sn) {
@@ -237,24 +199,15 @@ struct Leduc {
         hr = 0; nrn = 0; rc = 0; f0 = 0; f1 = 0; over = 0;
     }
 
-    // Game.init_game from a deal word (draw_deal, or the deal queue's entry: cs_dq.h dq_reset)
-    __device__ __forceinline__ void reset_from(uint32_t e0, uint32_t)
+    // Game.init_game from a deal word (draw_deal)
+    template <class Rng>
+    __device__ __forceinline__ void reset(Rng& rng)
     {
+        const uint32_t e0 = draw_deal(rng);
         h0 = (int)(e0 & 7u);
         h1 = (int)((e0 >> 3) & 7u);
         pub = (int)((e0 >> 6) & 7u);
         deal_blinds((int)((e0 >> 9) & 1u));
-    }
-    template <class Rng>
-    __device__ __forceinline__ void make_deal(Rng& rng, uint32_t&, uint32_t& e0, uint32_t& e1) const
-    {
-        e0 = draw_deal(rng);
-        e1 = 0u;
-    }
-    template <class Rng>
-    __device__ __forceinline__ void reset(Rng& rng)
-    {
-        reset_from(draw_deal(rng), 0u);
     }
 
     template <class Rng>

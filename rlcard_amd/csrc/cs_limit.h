@@ -25,34 +25,6 @@
 #pragma once
 #include "cs_device.h"
 
-#ifndef CS_LIMIT_STAGE_W
-#define CS_LIMIT_STAGE_W 128
-#endif
-#ifndef CS_LIMIT_STAGE_R
-#define CS_LIMIT_STAGE_R 100
-#endif
-#ifndef CS_LIMIT_RESTAGE_B
-#define CS_LIMIT_RESTAGE_B 8
-#endif
-#ifndef CS_LIMIT_MIN_WAVES
-#define CS_LIMIT_MIN_WAVES 4   // the LDS of a deal queue of 8 allows 4 blocks of 4 waves per CU
-#endif
-#ifndef CS_LIMIT_STAGE_RF
-#define CS_LIMIT_STAGE_RF 120   // batched restage: 2.70 -> 2.65 ms per 128-step launch (R 80 / RF 100 or 124 the same)
-#endif
-#ifndef CS_LIMIT_DQ_REGS
-#define CS_LIMIT_DQ_REGS 0
-#endif
-#ifndef CS_LIMIT_DQ_HBM
-#define CS_LIMIT_DQ_HBM 0   // rollout: the deal queue read and written in place in the env state (HBM), no LDS copy
-#endif
-#ifndef CS_LIMIT_SPARSE_OBS
-#define CS_LIMIT_SPARSE_OBS 1   // rollout obs rows through row_write_sparse (0: the expanded bitmap, RowWriter)
-#endif
-#ifndef CS_LIMIT_EPW
-#define CS_LIMIT_EPW 32
-#endif
-
 namespace cs {
 
 __device__ __forceinline__ int top_bit(uint32_t m) { return 31 - __builtin_clz(m); }
@@ -79,11 +51,8 @@ __device__ __forceinline__ void tally_card(int c, uint64_t& cnt, uint64_t& sm)
 // players: tallied once)
 // Branch-free form (the default): the rank-count bit planes come from the four suit masks by a bit-sliced adder
 // (count = a + b + c + d per rank bit), every category's tie-break ranks are computed and the category picks them,
-// so a wave's lanes never diverge on the hand category (the if-chain below executes the union of the categories its
-// lanes hold). Same values. CS_EVAL_BRANCHY=1: the if-chain.
-#ifndef CS_EVAL_BRANCHY
-#define CS_EVAL_BRANCHY 0
-#endif
+// so a wave's lanes never diverge on the hand category (an if-chain executes the union of the categories its lanes
+// hold: No-limit 3.09 -> 2.66 ms, Limit 2.61 -> 2.50 with this form).
 // highest set bit of m removed; its rank (31 - clz) in r (0xFFFFFFFF for m = 0, never packed)
 __device__ __forceinline__ uint32_t pop_top(uint32_t m, uint32_t& r)
 {
@@ -134,105 +103,19 @@ __device__ __forceinline__ uint32_t holdem_rank7_bf(uint64_t smp)
 
 __device__ inline uint32_t holdem_rank7(uint64_t cnt, uint64_t smp)
 {
-#ifdef CS_PROF_NO_EVAL   // profiling builds only: wrong showdowns, timing of the evaluator
+#if CS_PROF_NO_EVAL   // profiling builds only: wrong showdowns, timing of the evaluator
     return (uint32_t)(cnt ^ (cnt >> 32) ^ smp ^ (smp >> 29)) & 0xFFFFFFu;
 #endif
-    if constexpr (!CS_EVAL_BRANCHY) return holdem_rank7_bf(smp);
-    const uint32_t sm[4] = {(uint32_t)smp & 0x1FFFu, (uint32_t)(smp >> 16) & 0x1FFFu, (uint32_t)(smp >> 32) & 0x1FFFu,
-                            (uint32_t)(smp >> 48) & 0x1FFFu};
-    uint32_t m1 = 0, m2 = 0, m3 = 0, m4 = 0;
-#pragma unroll
-    for (int r = 0; r < 13; r++) {
-        const uint32_t n = (uint32_t)(cnt >> (4 * r)) & 15u;
-        m1 |= (n == 1u) << r; m2 |= (n == 2u) << r; m3 |= (n == 3u) << r; m4 |= (n == 4u) << r;
-    }
-    const uint32_t all = m1 | m2 | m3 | m4;
-    uint32_t fm = 0;
-#pragma unroll
-    for (int s = 0; s < 4; s++) fm = __popc(sm[s]) >= 5 ? sm[s] : fm;
-    uint32_t cat, v0 = 0, v1 = 0, v2 = 0, v3 = 0, v4 = 0;
-    const int sf = fm ? top_straight13(fm) : -1;
-    if (sf >= 0) {
-        cat = 9; v0 = sf;
-    } else if (m4) {
-        cat = 8; v0 = top_bit(m4); v1 = top_bit(all & ~(1u << v0));
-    } else if (m3 && (__popc(m3) >= 2 || m2)) {
-        cat = 7; v0 = top_bit(m3); v1 = top_bit((m3 & ~(1u << v0)) | m2);
-    } else if (fm) {
-        cat = 6;
-        uint32_t f = fm;
-        v0 = top_bit(f); f &= ~(1u << v0); v1 = top_bit(f); f &= ~(1u << v1); v2 = top_bit(f); f &= ~(1u << v2);
-        v3 = top_bit(f); f &= ~(1u << v3); v4 = top_bit(f);
-    } else if (top_straight13(all) >= 0) {
-        cat = 5; v0 = top_straight13(all);
-    } else if (m3) {
-        cat = 4; v0 = top_bit(m3);
-        uint32_t k = m1;
-        v1 = top_bit(k); k &= ~(1u << v1); v2 = top_bit(k);
-    } else if (__popc(m2) >= 2) {
-        cat = 3;
-        uint32_t p = m2;
-        v0 = top_bit(p); p &= ~(1u << v0); v1 = top_bit(p);
-        v2 = top_bit(all & ~(1u << v0) & ~(1u << v1));
-    } else if (m2) {
-        cat = 2; v0 = top_bit(m2);
-        uint32_t k = m1;
-        v1 = top_bit(k); k &= ~(1u << v1); v2 = top_bit(k); k &= ~(1u << v2); v3 = top_bit(k);
-    } else {
-        cat = 1;
-        uint32_t k = m1;
-        v0 = top_bit(k); k &= ~(1u << v0); v1 = top_bit(k); k &= ~(1u << v1); v2 = top_bit(k); k &= ~(1u << v2);
-        v3 = top_bit(k); k &= ~(1u << v3); v4 = top_bit(k);
-    }
-    return cat << 20 | v0 << 16 | v1 << 12 | v2 << 8 | v3 << 4 | v4;
+    (void)cnt;
+    return holdem_rank7_bf(smp);
 }
 
-// The nine dealt draws (random_interval(i), i = 51..43, mask 63) from the staged bytes without rejection loops: one
-// branch-free pass over the next 24 staged bytes (bit-field extract, compare with the current i) marks the accepted
-// bytes in a 24-bit mask, then the k-th set bit's byte is draw k. false: fewer than 28 staged bytes, or fewer than nine
-// acceptances among the 24 (the caller draws with interval(), same numbers).
-template <class Rng>
-__device__ __forceinline__ bool deal9_staged(Rng& rng, uint32_t (&j)[9])
-{
-    const uint32_t k0 = rng.staged_offset();
-    if (k0 >= rng.sn || rng.sn - k0 < 28u) return false;
-    const uint32_t* row = (const uint32_t*)(rng.stg + (k0 & ~3u));
-    const uint32_t sh = k0 & 3u;
-    uint32_t w[7];
-#pragma unroll
-    for (int q = 0; q < 7; q++) w[q] = row[q];
-    uint32_t i = 51, acc_mask = 0, n = 0;
-#pragma unroll
-    for (int q = 0; q < 6; q++) {
-        const uint32_t x = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh);   // staged bytes k0 + 4q ..
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const bool live = i >= 43u;
-            const uint32_t u = __builtin_amdgcn_ubfe(x, 8 * t, 6);
-            const bool acc = live && u <= i;
-            acc_mask |= acc ? 1u << (4 * q + t) : 0u;
-            i -= acc ? 1u : 0u;
-            n += live ? 1u : 0u;
-        }
-    }
-    if (i >= 43u) return false;
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
-        const uint32_t p = __builtin_ctz(acc_mask);
-        acc_mask &= acc_mask - 1u;
-        j[k] = rng.stg[k0 + p] & 63u;
-    }
-    rng.advance_by(n);
-    return true;
-}
-
-// deal9_staged without its 24-step dependency chain. For i = 51..43 (mask 63) a byte u = b & 63 is accepted for every
-// i if u <= 42, for none if u >= 52; only u in 43..51 ("maybe", 9/64 of the bytes) depends on i = 51 - (acceptances
-// before it). SWAR per dword gives the sure-accept and maybe masks of the 24 bytes; the maybes are then resolved in
-// order (a few per lane) from the popcount of the acceptances before each. Same bytes, same draws.
-#ifndef CS_DEAL9_SWAR
-#define CS_DEAL9_SWAR 1
-#endif
+// The nine dealt draws (random_interval(i), i = 51..43, mask 63) from the staged bytes without rejection loops or a
+// 24-step dependency chain. For i = 51..43 a byte u = b & 63 is accepted for every i if u <= 42, for none if u >= 52;
+// only u in 43..51 ("maybe", 9/64 of the bytes) depends on i = 51 - (acceptances before it). SWAR per dword gives the
+// sure-accept and maybe masks of the next 24 staged bytes; the maybes are then resolved in order (a few per lane) from
+// the popcount of the acceptances before each. Same bytes, same draws. false: fewer than 28 staged bytes, or fewer
+// than nine acceptances among the 24 (the caller draws with interval(), same numbers).
 template <class Rng>
 __device__ __forceinline__ bool deal9_swar(Rng& rng, uint32_t (&j)[9])
 {
@@ -273,35 +156,30 @@ __device__ __forceinline__ bool deal9_swar(Rng& rng, uint32_t (&j)[9])
     return true;
 }
 
-#ifndef CS_TRACK_SWAR
-#define CS_TRACK_SWAR 1   // 0: the JV table (per-swap position / card pairs looked up by the later swaps)
-#endif
 // The hold'em deal (limitholdem/dealer.py: shuffle the 52-card deck, deal_card = pop()) of a heads-up game: hole i ->
 // player i % 2, card i / 2 from deck[51 - i]; flop deck[47..45], turn deck[44], river deck[43]. Fisher-Yates fixes
-// position i at step i, and only deck[43..51] is ever dealt, so the first nine swaps are tracked (swap k writes card vj
-// to position 51 - k -- dealt card D[k] -- and card vi to position j: JV[k] = j | vi << 8, looked up by the later
-// swaps) and the other 42 only consume their draws. Out: holes packed p0c0 | p0c1 << 6 | p1c0 << 12 | p1c1 << 18,
-// board c0..c4 6 bits each. Registers only (the rollout kernels' occupancy is register-bound).
+// position i at step i, and only deck[43..51] is ever dealt, so the first nine swaps are tracked and the other 42 only
+// consume their draws. Out: holes packed p0c0 | p0c1 << 6 | p1c0 << 12 | p1c1 << 18, board c0..c4 6 bits each.
+// Registers only (the rollout kernels' occupancy is register-bound).
 template <class Rng>
 __device__ __forceinline__ void holdem_deal2(Rng& rng, uint32_t& holes, uint32_t& board)
 {
     uint32_t js[9];
     bool staged = false;
-#ifdef CS_PROF_NO_DEAL9   // profiling builds only: wrong deals, timing of the tracked draws
+#if CS_PROF_NO_DEAL9   // profiling builds only: wrong deals, timing of the tracked draws
 #pragma unroll
     for (int k = 0; k < 9; k++) js[k] = (uint32_t)k;
     rng.advance_by(12u);
     staged = true;
 #else
-    if constexpr (Rng::kMode == STAGE_LDS) staged = CS_DEAL9_SWAR ? deal9_swar(rng, js) : deal9_staged(rng, js);
+    if constexpr (Rng::kMode == STAGE_LDS) staged = deal9_swar(rng, js);
 #endif
     if (!staged) {
 #pragma unroll
         for (int k = 0; k < 9; k++) js[k] = rng.interval(51u - (uint32_t)k);
     }
-    uint32_t JV[9];
     uint32_t d0 = 0, d1 = 0;
-#if CS_TRACK_SWAR && !defined(CS_PROF_NO_TRACK)
+#if !CS_PROF_NO_TRACK
     // Dealt card k is the card at position 51 - k after the nine swaps (later swaps never touch positions >= 43): the
     // nine positions, four per word (bytes; 63 = unused, never matches), are traced back through the swaps q = 8 .. 0
     // -- a byte x in {i_q, j_q} flips by i_q ^ j_q; bytes < 64, so (b + 0x7F) sets bit 7 exactly when b != 0 -- and end
@@ -329,32 +207,14 @@ __device__ __forceinline__ void holdem_deal2(Rng& rng, uint32_t& holes, uint32_t
             else d1 |= v << (6 * (k - 4));
         }
     }
-    if (false)
-#endif
-#ifdef CS_PROF_NO_TRACK   // profiling builds only: wrong deals, timing of the swap tracking
+#else   // profiling builds only (cs_prof.h): the draws as the cards
 #pragma unroll
     for (int k = 0; k < 9; k++) {
         if (k < 4) d0 |= js[k] << (6 * k);
         else d1 |= js[k] << (6 * (k - 4));
     }
-    if (false)
 #endif
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
-        const uint32_t i = 51 - k, j = js[k];
-        uint32_t vi = i, vj = j;
-#pragma unroll
-        for (int q = 0; q < k; q++) {   // oldest -> newest: the newest write to a position wins
-            const uint32_t jq = JV[q] & 255u, vq = JV[q] >> 8;
-            vi = jq == i ? vq : vi;
-            vj = jq == j ? vq : vj;
-        }
-        JV[k] = j | (vi << 8);
-        constexpr int F0[4] = {0, 12, 6, 18};   // hole i -> player i % 2, card i / 2
-        if (k < 4) d0 |= vj << F0[k < 4 ? k : 0];
-        else d1 |= vj << (6 * (k - 4));
-    }
-#ifdef CS_PROF_NO_SKIP   // profiling builds only: wrong streams, timing of the skip scan
+#if CS_PROF_NO_SKIP   // profiling builds only: wrong streams, timing of the skip scan
     rng.advance_by(60u);
 #else
     rng.skip_intervals(42u);   // deck positions 42..1 are never dealt: only the words they consume matter
@@ -363,9 +223,6 @@ __device__ __forceinline__ void holdem_deal2(Rng& rng, uint32_t& holes, uint32_t
     board = d1;
 }
 
-#ifndef CS_SHOWDOWN_SERIAL
-#define CS_SHOWDOWN_SERIAL 1
-#endif
 // the showdown of a heads-up deal when both players stay in (Judger.judge_game -> compare_hands, judger.py:11-108,
 // utils.py): bit 0 = player 0 wins or ties, bit 1 = player 1. It depends on the deal alone: no-limit evaluates it when
 // the deal is drawn (in the rollout's lockstep deal passes) and keeps it in the state; limit at the game's end.
@@ -380,13 +237,11 @@ __device__ __forceinline__ uint32_t holdem_showdown(uint32_t holes, uint32_t boa
     tally_card((int)((holes >> 12) & 63u), c1, s1);
     tally_card((int)((holes >> 18) & 63u), c1, s1);
     uint32_t v0 = holdem_rank7(c0, s0);
-#if CS_SHOWDOWN_SERIAL
     // the second evaluation's inputs pass through an empty asm with the first result: the two branch-free evaluations
     // run one after the other instead of interleaved (half the live temporaries: occupancy, no spills)
     uint32_t s1lo = (uint32_t)s1, s1hi = (uint32_t)(s1 >> 32);
     asm volatile("" : "+v"(v0), "+v"(s1lo), "+v"(s1hi));
     s1 = (uint64_t)s1hi << 32 | s1lo;
-#endif
     const uint32_t v1 = holdem_rank7(c1, s1);
     return (uint32_t)(v0 >= v1) | (uint32_t)(v1 >= v0) << 1;
 }
@@ -399,12 +254,9 @@ __device__ __forceinline__ uint32_t holdem_showdown(uint32_t holes, uint32_t boa
 // drawn << XB, dealer << XB + 1, draws[8:7] of slot k << XB + 2 + 2 k; CB = log2(DQ) + 1, XB = 2 CB - 1: DQ 4 -> 3, 5;
 // DQ 8 -> 4, 7) and DQ entries of two words (e0 = holes | seat bit << 24 | draws[6:0] << 25, e1 = board | showdown
 // << 30; draws = MT words the deal consumed, for the host's stream position, saturating at 511).
-#ifndef CS_DEAL_QUEUE
-#define CS_DEAL_QUEUE 8   // 8 vs 4 (LDS queue): 0.39 vs 0.46 deal passes per wave-step (simulated), the pass costs ~1 200
-                          // wave-instructions; with 4 waves per SIMD instead of 5: Limit -2.5 %, No-limit -0.7 %
-#endif
-constexpr int HOLDEM_DQ = CS_DEAL_QUEUE;
-static_assert(HOLDEM_DQ == 0 || HOLDEM_DQ == 2 || HOLDEM_DQ == 4 || HOLDEM_DQ == 8, "deal queue: power-of-two ring");
+// Depth 8 vs 4 (LDS queue): 0.39 vs 0.46 deal passes per wave-step (simulated), the pass costs ~1 200
+// wave-instructions; with 4 waves per SIMD instead of 5: Limit -2.5 %, No-limit -0.7 %.
+constexpr int HOLDEM_DQ = 8;
 constexpr int HOLDEM_DQ_WORDS = HOLDEM_DQ > 0 ? 1 + 2 * HOLDEM_DQ : 0;
 constexpr int DQ_CB = HOLDEM_DQ == 8 ? 4 : HOLDEM_DQ == 4 ? 3 : 2;   // count bits (0..DQ)
 constexpr int DQ_XB = 2 * DQ_CB - 1;                                // first bit after count and head
@@ -413,20 +265,18 @@ static_assert(DQ_XB + 2 + 2 * HOLDEM_DQ <= 32, "deal queue header fits a word");
 struct Limit {
     static constexpr int GW = 4;                        // game words; the deal queue follows
     static constexpr int DQ = HOLDEM_DQ;
-    static constexpr bool DQ_REGS = CS_LIMIT_DQ_REGS;          // rollout: queue in registers, else LDS
-    static constexpr bool DQ_HBM = CS_LIMIT_DQ_HBM;            // rollout: queue in place in the state (HBM)
     static constexpr int OBS = 72, A = 4, P = 2, LB = 1, WORDS = GW + HOLDEM_DQ_WORDS, ACTION_BYTES = 1;
     static constexpr int NB = 3;
     static constexpr bool RING = true;          // MT stream as the byte ring (cs_ring.h)
     static constexpr bool RAW_OBS = false;
     static constexpr int SCRATCH_WORDS = 0;
     // MT staging (see MtLaneT)
-    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = CS_LIMIT_STAGE_W, STAGE_PAD = 8, STAGE_R = CS_LIMIT_STAGE_R;
-    static constexpr int STAGE_RF = CS_LIMIT_STAGE_RF;    // batch restage threshold (ring_restage_wave)
-    static constexpr int RESTAGE_B = CS_LIMIT_RESTAGE_B;  // lanes restaged per pass (loads in flight)
-    static constexpr int MIN_WAVES = CS_LIMIT_MIN_WAVES;  // 4 waves/SIMD (LDS-bound with the 8-deal queue; at a 4-deal
-                                                          // queue 5 beat 4 and 6, which spilled 40 VGPRs)
-    static constexpr int EPW = CS_LIMIT_EPW;   // rollout envs per wave: 262 144 envs need half-full waves (lane_ctx)
+    static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_PAD = 8, STAGE_R = 100;
+    static constexpr int STAGE_RF = 120;  // batch restage threshold (ring_restage_wave): 2.70 -> 2.65 ms per 128 steps
+    static constexpr int RESTAGE_B = 8;   // lanes restaged per pass (loads in flight)
+    static constexpr int MIN_WAVES = 4;   // 4 waves/SIMD (LDS-bound with the 8-deal queue; at a 4-deal queue 5 beat 4
+                                          // and 6, which spilled 40 VGPRs)
+    static constexpr int EPW = 32;   // rollout envs per wave: 262 144 envs need half-full waves (lane_ctx)
     static constexpr bool LANE_OPAQUE = false;   // k_rollout: lane id not made opaque per step (cs_skeleton.h LaneOpaque)
     static constexpr int REFILL_K = 2;   // stale blocks twisted per pass (see mt_refill_wave)
     __device__ __forceinline__ void bind(uint32_t*, const GameParams&) {}
@@ -490,7 +340,7 @@ struct Limit {
 
     // the same row as the byte positions of its 11 ones (row_write_sparse): the two holes, the five board cards (not
     // yet public: the first hole again), obs byte 52 + 5 i + raise count of round i (i = 0..3)
-    static constexpr int SPARSE_K = CS_LIMIT_SPARSE_OBS ? 11 : 0;
+    static constexpr int SPARSE_K = 11;
     __device__ __forceinline__ uint32_t observe_pos(int player, uint32_t (&pos)[11]) const
     {
         const int r = rc(), npub = r == 0 ? 0 : (r == 1 ? 3 : (r == 2 ? 4 : 5));

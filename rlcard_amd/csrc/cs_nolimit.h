@@ -34,32 +34,11 @@
 #include "cs_device.h"
 #include "cs_limit.h"
 
-#ifndef CS_NOLIMIT_STAGE_RF
-#define CS_NOLIMIT_STAGE_RF 100   // = STAGE_R (120 measured the same: 2.99 ms per 128-step launch)
-#endif
-#ifndef CS_NOLIMIT_DQ_REGS
-#define CS_NOLIMIT_DQ_REGS 0
-#endif
-#ifndef CS_NOLIMIT_DQ_HBM
-#define CS_NOLIMIT_DQ_HBM 0
-#endif
-#ifndef CS_NOLIMIT_SPARSE_OBS
-#define CS_NOLIMIT_SPARSE_OBS 1   // rollout obs rows through row_write_sparse (0: RowWriterRaw of the expanded row)
-#endif
-#ifndef CS_NOLIMIT_EPW
-#define CS_NOLIMIT_EPW 32
-#endif
-#ifndef CS_NOLIMIT_MIN_WAVES
-#define CS_NOLIMIT_MIN_WAVES 4   // LDS-bound at 4 blocks per CU with the 8-deal queue
-#endif
-
 namespace cs {
 
 struct Nolimit {
     static constexpr int GW = 4;                        // game words; the deal queue follows (cs_limit.h)
     static constexpr int DQ = HOLDEM_DQ;
-    static constexpr bool DQ_REGS = CS_NOLIMIT_DQ_REGS;          // rollout: queue in registers, else LDS
-    static constexpr bool DQ_HBM = CS_NOLIMIT_DQ_HBM;            // rollout: queue in place in the state (HBM)
     static constexpr int OBS = 54, A = 5, P = 2, LB = 1, WORDS = GW + HOLDEM_DQ_WORDS, ACTION_BYTES = 1;
     static constexpr int NB = 14;               // raw obs bytes, four per word (RowWriterRaw)
     static constexpr bool RING = true;          // MT stream as the byte ring (cs_ring.h)
@@ -67,10 +46,10 @@ struct Nolimit {
     static constexpr int SCRATCH_WORDS = 0;
     // MT staging and launch shape as limit hold'em (same deal: ~72 draws per game)
     static constexpr int STAGE_MODE = STAGE_LDS, STAGE_W = 128, STAGE_PAD = 8, STAGE_R = 100;
-    static constexpr int STAGE_RF = CS_NOLIMIT_STAGE_RF;  // batch restage threshold (ring_restage_wave)
+    static constexpr int STAGE_RF = 100;  // batch restage threshold (ring_restage_wave) = STAGE_R (120 the same)
     static constexpr int RESTAGE_B = 8;
-    static constexpr int MIN_WAVES = CS_NOLIMIT_MIN_WAVES;
-    static constexpr int EPW = CS_NOLIMIT_EPW;
+    static constexpr int MIN_WAVES = 4;   // LDS-bound at 4 blocks per CU with the 8-deal queue
+    static constexpr int EPW = 32;
     static constexpr bool LANE_OPAQUE = false;   // k_rollout: lane id not made opaque per step (cs_skeleton.h LaneOpaque)
     static constexpr bool REWARD_OPAQUE = true;  // k_rollout: keeps the reward rows' nontemporal hint (RewardOpaque)
     static constexpr int REFILL_K = 2;
@@ -144,7 +123,7 @@ struct Nolimit {
 
     // the same row as the byte positions of its 7 card ones (row_write_sparse: the two holes, the public board cards,
     // the first hole again for the others) and its last two bytes (my chips | the max chips << 8), returned
-    static constexpr int SPARSE_K = CS_NOLIMIT_SPARSE_OBS ? 7 : 0;
+    static constexpr int SPARSE_K = 7;
     __device__ __forceinline__ uint32_t observe_pos(int player, uint32_t (&pos)[7]) const
     {
         const int r = rc(), npub = r == 0 ? 0 : (r + 2 < 5 ? r + 2 : 5);

@@ -28,10 +28,10 @@
 
 namespace cs {
 
-// Ring slots (CS_RING_SLOTS, cs_engine.h): a refill twists SLOTS - 1 blocks in a row from one read of wbuf and writes
+// Ring slots (RING_SLOTS_HOST, cs_engine.h): a refill twists SLOTS - 1 blocks in a row from one read of wbuf and writes
 // wbuf back once, so the block-word traffic per draw is 2 x 2 496 B / ((SLOTS - 1) x 624): 4 slots 2.67 B/draw, 8 slots
 // 1.14 B/draw (per env 624 + SLOTS x 156 u32 = RING_ENV_WORDS).
-constexpr int RING_SLOTS = CS_RING_SLOTS;
+constexpr int RING_SLOTS = RING_SLOTS_HOST;
 static_assert(RING_SLOTS == 4 || RING_SLOTS == 8 || RING_SLOTS == 16, "ring slots: a power of two, position < 2^14");
 constexpr uint32_t SLOT_MASK = (uint32_t)RING_SLOTS - 1u;
 constexpr int RING_GEN = RING_SLOTS - 1;        // blocks generated per refill
@@ -111,33 +111,19 @@ __device__ __attribute__((noinline)) void ring_gen_serial(uint32_t* wbuf, uint32
 
 // Block words in registers, word k = 64c + lane in o[c] (c = 9 holds words 576..623 in lanes 0..47). One twist:
 //   new[k] = mix(old[k], old[k+1] | new[0] (k = 623), old[k+397] (k < 227) | new[k-227])
-// with the cross-lane operands fetched by ds_bpermute; n[c] only depends on n[c-4], n[c-3] and n[0] (computed first).
-// CS_TWIST_DPP: the k+1 operand (the next lane) through a DPP wavefront shift (wave_shl:1, a VALU modifier) instead of
-// a ds_bpermute round trip through the LDS crossbar
-#ifndef CS_TWIST_DPP
-#define CS_TWIST_DPP 1
-#endif
+// with the cross-lane operands fetched by ds_bpermute, but the k+1 operand (the next lane) through a DPP wavefront
+// shift (wave_shl:1, a VALU modifier) instead of a ds_bpermute round trip through the LDS crossbar; n[c] only depends
+// on n[c-4], n[c-3] and n[0] (computed first).
 __device__ __forceinline__ void twist_regs(const uint32_t (&o)[10], uint32_t (&n)[10], int lane)
 {
-    const int l1 = (lane + 1) & 63, l13 = (lane + 13) & 63, l29 = (lane + 29) & 63;
-    (void)l1;
+    const int l13 = (lane + 13) & 63, l29 = (lane + 29) & 63;
 #pragma unroll
     for (int c = 0; c < 10; c++) {
-        uint32_t nxt;
-        if constexpr (CS_TWIST_DPP != 0) {
-            // wave_shl:1 without bound_ctrl: lane 63 has no source lane and keeps `old` -- the wrap word (the next
-            // chunk's lane 0) goes in as `old`, so the shift needs no select (chunk 9 wraps at lane 47: below)
-            const int old = c < 9 ? (int)__builtin_amdgcn_readlane(o[c < 9 ? c + 1 : 9], 0) : 0;
-            nxt = (uint32_t)__builtin_amdgcn_update_dpp(old, (int)o[c], 0x130, 0xF, 0xF, false);
-        } else {
-            nxt = shfl(o[c], l1);
-        }
-        if (c < 9) {
-            if constexpr (CS_TWIST_DPP == 0) {
-                const uint32_t wrap = __builtin_amdgcn_readlane(o[c + 1], 0);
-                nxt = lane == 63 ? wrap : nxt;
-            }
-        } else {
+        // wave_shl:1 without bound_ctrl: lane 63 has no source lane and keeps `old` -- the wrap word (the next chunk's
+        // lane 0) goes in as `old`, so the shift needs no select (chunk 9 wraps at lane 47: below)
+        const int old = c < 9 ? (int)__builtin_amdgcn_readlane(o[c < 9 ? c + 1 : 9], 0) : 0;
+        uint32_t nxt = (uint32_t)__builtin_amdgcn_update_dpp(old, (int)o[c], 0x130, 0xF, 0xF, false);
+        if (c == 9) {
             const uint32_t n0 = __builtin_amdgcn_readlane(n[0], 0);
             nxt = lane == 47 ? n0 : nxt;
         }
@@ -158,27 +144,9 @@ __device__ __forceinline__ void twist_regs(const uint32_t (&o)[10], uint32_t (&n
     }
 }
 
-// stream traffic cache policy for A/B runs: CS_RING_NT bit 0 = nontemporal loads (refill's block words, restage's
-// ring bytes), bit 1 = nontemporal stores (ring bytes, block words)
-#ifndef CS_RING_NT
-#define CS_RING_NT 0
-#endif
-__device__ __forceinline__ uint32_t ring_ld(const gu32* p)
-{
-    if constexpr ((CS_RING_NT & 1) != 0) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-__device__ __forceinline__ void ring_st(gu32* p, uint32_t v)
-{
-    if constexpr ((CS_RING_NT & 2) != 0) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
-
-// ring bytes of a refill: every lane stores its word's byte (one global_store_byte per 64 words) instead of packing
-// four lanes' bytes with DPP moves into a dword store by every fourth lane
-#ifndef CS_RING_BYTE_ST
-#define CS_RING_BYTE_ST 1
-#endif
+// stream traffic: default-policy loads and stores (nontemporal ones measured slower for Leduc)
+__device__ __forceinline__ uint32_t ring_ld(const gu32* p) { return *p; }
+__device__ __forceinline__ void ring_st(gu32* p, uint32_t v) { *p = v; }
 
 // Wave-cooperative refill of one env: blocks L+1..L+3 from wbuf (block L, slot lat). All 64 lanes must call.
 __device__ __forceinline__ void ring_gen_wave(gu32* wbuf, uint32_t lat, int lane, uint32_t phx = 0)
@@ -201,18 +169,9 @@ __device__ __forceinline__ void ring_gen_wave(gu32* wbuf, uint32_t lat, int lane
         const uint32_t slot = (lat + (uint32_t)b) & SLOT_MASK;
 #pragma unroll
         for (int c = 0; c < 10; c++) {
-            if constexpr (CS_RING_BYTE_ST) {
-                if (c < 9 || lane < 48)
-                    ((gu8*)(ring + slot * (MT_N / 4)))[64 * c + lane] = (uint8_t)mt_temper_lo8(n[c]);
-            } else {
-                const int t = (int)(mt_temper(n[c]) & 255u);
-                const uint32_t t1 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x101, 0xF, 0xF, true);  // row_shl:1
-                const uint32_t t2 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x102, 0xF, 0xF, true);  // row_shl:2
-                const uint32_t t3 = (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x103, 0xF, 0xF, true);  // row_shl:3
-                if ((lane & 3) == 0 && (c < 9 || lane < 48))
-                    ring_st(ring + slot * (MT_N / 4) + 16 * c + (lane >> 2),
-                            (uint32_t)t | (t1 << 8) | (t2 << 16) | (t3 << 24));
-            }
+            // every lane stores its word's byte (one global_store_byte per 64 words): faster than packing four
+            // lanes' bytes with DPP moves into a dword store by every fourth lane
+            if (c < 9 || lane < 48) ((gu8*)(ring + slot * (MT_N / 4)))[64 * c + lane] = (uint8_t)mt_temper_lo8(n[c]);
             o[c] = n[c];
         }
     }

@@ -46,22 +46,15 @@ __device__ inline void mt_init_by_array(uint32_t* mt, const uint32_t* key, int k
     mt[0] = 0x80000000u;
 }
 
-#ifndef CS_WID_UNIFORM
-#define CS_WID_UNIFORM 1   // lane_ctx: the wave index through readfirstlane (A/B knob)
-#endif
-// k_rollout: the lane id made opaque at every step (per game, G::LANE_OPAQUE, default on; CS_LANE_OPAQUE = 0 / 1
-// overrides every game for A/B builds). Round 5, same box: Limit 8.18 -> 8.07 ms and No-limit 9.33 -> 9.10 without
-// it, Blackjack 20.62 -> 20.89 and Leduc even
-#ifndef CS_LANE_OPAQUE
-#define CS_LANE_OPAQUE -1
-#endif
+// k_rollout: the lane id made opaque at every step (per game, G::LANE_OPAQUE, default on). Round 5, same box: Limit
+// 8.18 -> 8.07 ms and No-limit 9.33 -> 9.10 without it, Blackjack 20.62 -> 20.89 and Leduc even
 template <class G, class = void>
 struct LaneOpaque {
-    static constexpr bool value = CS_LANE_OPAQUE != 0;
+    static constexpr bool value = true;
 };
 template <class G>
 struct LaneOpaque<G, std::void_t<decltype(G::LANE_OPAQUE)>> {
-    static constexpr bool value = CS_LANE_OPAQUE >= 0 ? CS_LANE_OPAQUE == 1 : G::LANE_OPAQUE;
+    static constexpr bool value = G::LANE_OPAQUE;
 };
 struct LaneCtx {
     int lane, wid;
@@ -72,13 +65,13 @@ struct LaneCtx {
 
 // EPW envs per wave (lanes >= EPW idle): 64 everywhere but the rollouts of games with too few envs to fill the chip
 // (Limit's 262 144 envs are 4 waves per SIMD at 64 per wave; half-full waves double that -- the step is latency-bound)
-template <int EPW = WAVE, bool XCD = false>
+template <int EPW = WAVE>
 __device__ __forceinline__ LaneCtx lane_ctx(int64_t n)
 {
     LaneCtx c;
     c.lane = threadIdx.x & (WAVE - 1);
-    c.wid = CS_WID_UNIFORM ? __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE) : (int)(threadIdx.x / WAVE);   // wave-uniform: wave_first lives in SGPRs
-    const int64_t bx = XCD ? (int64_t)xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;   // cs_device.h
+    c.wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // wave-uniform: wave_first lives in SGPRs
+    const int64_t bx = (int64_t)blockIdx.x;   // (XCD-aware block order, cs_device.h xcd_block: +2 % for Leduc)
     c.wave_first = (bx * WAVES_PER_BLOCK + c.wid) * EPW;
     c.env = c.wave_first + c.lane;
     const int64_t left = n - c.wave_first;
@@ -159,28 +152,6 @@ struct SparseK<G, std::void_t<decltype(G::SPARSE_K)>> {
     static constexpr int value = G::SPARSE_K > 0 ? G::SPARSE_K : 1;
 };
 
-// k_rollout's order inside a step, per game (G::STORES_LAST, default 0; CS_STORES_LAST = 0 / 1 overrides every game
-// for A/B builds): 1 = every trajectory store of the step after its refill / restage loads -- on gfx950 one counter
-// (vmcnt) tracks loads and stores in issue order, so a load issued after the rows waits until every row store is
-// acknowledged, a drain whose length is the HBM write latency of the moment, which depends on where the trajectory
-// landed in HBM (Leduc 5.1 -> 4.1 ms on physically contiguous trajectories); 0 = each row stored
-// where it is produced: every game (Leduc 4.22 vs 4.51 ms on torch allocations once the stores-first step compiled as
-// well as round 4's; Limit 8.1 vs 8.35 -- VALU-bound, the rows' live ranges cost more)
-#ifndef CS_STORES_LAST
-#define CS_STORES_LAST -1
-#endif
-#ifndef CS_ROLLOUT_XCD
-#define CS_ROLLOUT_XCD 0   // k_rollout blocks in XCD-aware order (cs_device.h xcd_block); A/B knob
-#endif
-template <class G, class = void>
-struct StoresLast {
-    static constexpr bool value = CS_STORES_LAST == 1;
-};
-template <class G>
-struct StoresLast<G, std::void_t<decltype(G::STORES_LAST)>> {
-    static constexpr bool value = CS_STORES_LAST >= 0 ? CS_STORES_LAST == 1 : G::STORES_LAST;
-};
-
 template <class G>
 __device__ __forceinline__ void emit_legal(uint8_t* legal, int64_t row, uint64_t lg)
 {
@@ -188,23 +159,17 @@ __device__ __forceinline__ void emit_legal(uint8_t* legal, int64_t row, uint64_t
     for (int k = 0; k < G::LB; k++) out_store(legal + row * G::LB + k, (uint8_t)(lg >> (8 * k)));
 }
 
-#ifndef CS_REWARD_NT
-#define CS_REWARD_NT 1   // 0: default-policy 8-B reward stores (A/B knob)
-#endif
-// the 8-B reward row's value made opaque before its nontemporal store (per game, G::REWARD_OPAQUE, default off;
-// CS_REWARD_OPAQUE = 0 / 1 overrides every game): without it the optimizer may split the store back into two float
-// stores and drop the nontemporal hint on the way (No-limit's rollout); with it where the hint survives anyway
-// (Leduc, Limit) the step schedules worse (Leduc 4.23 -> 4.48 ms, round 5)
-#ifndef CS_REWARD_OPAQUE
-#define CS_REWARD_OPAQUE -1
-#endif
+// the 8-B reward row's value made opaque before its nontemporal store (per game, G::REWARD_OPAQUE, default off):
+// without it the optimizer may split the store back into two float stores and drop the nontemporal hint on the way
+// (No-limit's rollout); with it where the hint survives anyway (Leduc, Limit) the step schedules worse (Leduc 4.23 ->
+// 4.48 ms, round 5)
 template <class G, class = void>
 struct RewardOpaque {
-    static constexpr bool value = CS_REWARD_OPAQUE == 1;
+    static constexpr bool value = false;
 };
 template <class G>
 struct RewardOpaque<G, std::void_t<decltype(G::REWARD_OPAQUE)>> {
-    static constexpr bool value = CS_REWARD_OPAQUE >= 0 ? CS_REWARD_OPAQUE == 1 : G::REWARD_OPAQUE;
+    static constexpr bool value = G::REWARD_OPAQUE;
 };
 template <class G>
 __device__ __forceinline__ void emit_reward(float* reward, int64_t row, const float (&r)[G::P])
@@ -212,62 +177,10 @@ __device__ __forceinline__ void emit_reward(float* reward, int64_t row, const fl
     if constexpr (G::P == 2) {
         uint64_t v = (uint64_t)__float_as_uint(r[0]) | (uint64_t)__float_as_uint(r[1]) << 32;
         if constexpr (RewardOpaque<G>::value) asm volatile("" : "+v"(v));
-        if constexpr (CS_REWARD_NT) out_store((uint64_t*)(reward + row * 2), v);
-        else *(uint64_t*)(reward + row * 2) = v;
+        out_store((uint64_t*)(reward + row * 2), v);
     } else {
 #pragma unroll
         for (int k = 0; k < G::P; k++) reward[row * G::P + k] = r[k];
-    }
-}
-
-// Two-player reward rows (8 B) of the rollout as 16-B stores: even lanes take their odd neighbour's pair (one DPP
-// row shift) and store both rows at once. All lanes call (invalid lanes hold zeros). Per game (G::REWARD_PAIRS,
-// default off; CS_REWARD_PAIRS = 0 / 1 / 2 overrides every two-player game for A/B builds); off: one 8-B store per
-// lane. Measured: the 8-B nontemporal reward rows cost ~1.8x their bytes in WRITE_SIZE (Leduc 1.6 GB per
-// launch); pairs bring WRITE_SIZE to the algorithmic bytes. With the rows stored where they were produced they ran
-// slower (4.59 -> 4.78 ms Leduc, 2.67 -> 2.80 Limit, round 2); with Leduc's rows after the step's loads (round 5,
-// StoresLast) 3.95 -> 3.86 ms, but that form is off (see StoresLast): off everywhere.
-#ifndef CS_REWARD_PAIRS
-#define CS_REWARD_PAIRS -1
-#endif
-template <class G, class = void>
-struct RewardPairsOf {
-    static constexpr int value = 0;
-};
-template <class G>
-struct RewardPairsOf<G, std::void_t<decltype(G::REWARD_PAIRS)>> {
-    static constexpr int value = G::REWARD_PAIRS ? 1 : 0;
-};
-template <class G>
-struct RewardPairs {
-    static constexpr int mode = CS_REWARD_PAIRS >= 0 ? CS_REWARD_PAIRS : RewardPairsOf<G>::value;
-    static constexpr bool value = mode != 0 && G::P == 2;
-};
-// CS_REWARD_PAIRS=2: the wave's 2 x EPW reward dwords transposed so that lane l stores dword l (and 64 + l): fully
-// coalesced 4-B stores (4 ds_bpermute per step)
-template <int EPW>
-__device__ __forceinline__ void emit_reward_t(float* reward, int64_t rowbase, const float (&r)[2], const LaneCtx& c)
-{
-    const uint32_t a0 = __float_as_uint(r[0]), a1 = __float_as_uint(r[1]);
-    uint32_t* dst = (uint32_t*)(reward + (rowbase + c.wave_first) * 2);
-#pragma unroll
-    for (int h = 0; h < (2 * EPW + WAVE - 1) / WAVE; h++) {
-        const int d = h * WAVE + c.lane, src = d >> 1;
-        const uint32_t x = __builtin_amdgcn_ds_bpermute(src << 2, (int)a0), y = __builtin_amdgcn_ds_bpermute(src << 2, (int)a1);
-        if (d < 2 * EPW && src < c.nvalid) out_store(dst + d, (d & 1) ? y : x);
-    }
-}
-template <int P>
-__device__ __forceinline__ void emit_reward_pairs(float* reward, int64_t rowbase, const float (&r)[P],
-                                                  const LaneCtx& c)
-{
-    const uint32_t a0 = __float_as_uint(r[0]), a1 = __float_as_uint(r[P > 1 ? 1 : 0]);
-    const uint32_t b0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a0, 0x101, 0xF, 0xF, true);   // row_shl:1
-    const uint32_t b1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a1, 0x101, 0xF, 0xF, true);
-    if ((c.lane & 1) == 0 && c.valid) {
-        float* dst = reward + (rowbase + c.env) * 2;
-        if (c.lane + 1 < c.nvalid) out_store16((uint4*)dst, make_uint4(a0, a1, b0, b1));
-        else out_store((uint64_t*)dst, (uint64_t)a0 | (uint64_t)a1 << 32);
     }
 }
 
@@ -574,9 +487,8 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
     uint8_t* const sbuf = args.sbuf;
     CS_SMEM_ROWS(G, G::EPW);
     __shared__ __attribute__((aligned(16))) uint8_t stage[WAVES_PER_BLOCK][StageBytes<G>::value];
-    const LaneCtx c = lane_ctx<G::EPW, CS_ROLLOUT_XCD != 0>(n);
+    const LaneCtx c = lane_ctx<G::EPW>(n);
     RingLane<G::STAGE_MODE> m = ring_lane<G::STAGE_MODE>(mt, ctl, c);
-    constexpr bool SL = StoresLast<G>::value;
     // MT staging needs both blocks valid at every restage, i.e. the cooperative refill (flag bit 0 off);
     // flag bit 1 disables it (one global load per draw) for A/B runs and fallback-path tests
     const bool staged = !(flags & 3);
@@ -595,23 +507,15 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
             stage_rows_copy<G::STAGE_W, G::STAGE_PAD>(stage[c.wid], rows, c.lane, c.nvalid, true);
         }
     }
-    // the deal queues of the wave's envs for the launch: in registers, or in LDS (DQW consecutive words per lane:
-    // odd stride), per the game's DQ_REGS
-    // or in place in the env state in HBM (per the game's DQ_HBM: no copy, no LDS; lanes without an env never touch it)
+    // the deal queues of the wave's envs for the launch in LDS (DQW consecutive words per lane: odd stride)
     constexpr int DQ = DqOf<G>::value, DQW = DqOf<G>::words;
-    constexpr bool QREGS = DqOf<G>::regs, QHBM = DqOf<G>::hbm;
-    __shared__ uint32_t dql[DQ > 0 && !QREGS && !QHBM ? WAVES_PER_BLOCK * G::EPW * DQW : 1];
-    using QV = std::conditional_t<QREGS, DqRegs<DQW ? DQW : 1>, DqMem>;
-    QV q{};
+    __shared__ uint32_t dql[DQ > 0 ? WAVES_PER_BLOCK * G::EPW * DQW : 1];
+    DqMem q{};
     if constexpr (DQ > 0) {
-        if constexpr (QHBM) {
-            q = DqMem{st + (int64_t)G::GW * n + (c.valid ? c.env : 0), n};
-        } else {
-            if constexpr (!QREGS) q = DqMem{dql + (c.wid * G::EPW + (c.lane < G::EPW ? c.lane : 0)) * DQW, 1};
-            if (c.valid) {
+        q = DqMem{dql + (c.wid * G::EPW + (c.lane < G::EPW ? c.lane : 0)) * DQW, 1};
+        if (c.valid) {
 #pragma unroll
-                for (int w = 0; w < DQW; w++) q.set(w, st[(int64_t)(G::GW + w) * n + c.env]);
-            }
+            for (int w = 0; w < DQW; w++) q.set(w, st[(int64_t)(G::GW + w) * n + c.env]);
         }
     }
     G g;
@@ -627,10 +531,7 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
     refill<G>(m, c.lane, flags & 1);
     if (staged) restage<G>(m, stage[c.wid], c.lane, c.valid);
     PolicyRng pol;
-#ifndef CS_GENV_HOIST
-#define CS_GENV_HOIST 1   // the stores-first step: the policy counter's env id computed once, before the loop (A/B knob)
-#endif
-    [[maybe_unused]] const uint64_t genv0 = args.env_base + (uint64_t)c.env;
+    const uint64_t genv0 = args.env_base + (uint64_t)c.env;   // the policy counter's env id
     for (int t = 0; t < T; t++) {
         const RolloutArgs& A = arg();
         // the lane id made opaque at every step, so lane-derived values (env id, row and LDS addresses) are recomputed
@@ -656,158 +557,39 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
         const uint64_t lg = g.legal();
         uint32_t bits[G::NB];
         g.observe(p, bits);
-#ifndef CS_SF_PLAIN
-#define CS_SF_PLAIN 1   // A/B knob: the stores-first step written out in place (1) or through the lambdas below (0)
-#endif
-        if constexpr (!SL && CS_SF_PLAIN != 0) {
-            // each row stored where it is produced. Written out rather than through the stores-last path's lambdas:
-            // the same operations in that form compiled to a schedule 6 % slower for Leduc in every placement
-            // (round 5, same-box A/B against the round-4 build)
-            const uint64_t genv = CS_GENV_HOIST ? genv0 : A.env_base + (uint64_t)(c.wave_first + cl.lane);
-            const uint32_t pr = pol.at(seed, genv, t0 + (uint64_t)t, t == 0);
-            int a;
-            if constexpr (G::A <= 8) a = pick_legal_small<G::A>((uint32_t)lg, pr);
-            else a = G::A <= 32 ? pick_legal32((uint32_t)lg, pr) : pick_legal(lg, pr);
-#ifndef CS_PROF_NO_OBS
-            if constexpr (SparseObs<G>::value) {
-                uint32_t pos[SparseK<G>::value];
-                const uint32_t tail = g.observe_pos(p, pos);
-                row_write_sparse<G::OBS, G::EPW, SparseK<G>::value, G::RAW_OBS>(
-                    lds[c.wid], pos, obs + (rowbase + c.wave_first) * G::OBS, cl.lane, c.nvalid, !(flags & 4), tail);
-            } else {
-                emit_obs<G, G::EPW>(lds[c.wid], bits, obs, rowbase + c.wave_first, flags, cl);
-            }
-#endif
-            uint32_t zr = 0;   // see below (CS_ZERO_OPAQUE)
-            asm volatile("" : "+v"(zr));
-            float r[G::P];
-#pragma unroll
-            for (int k = 0; k < G::P; k++) r[k] = __uint_as_float(zr);
-            bool done = false;
-            if (c.valid) {
-                const int64_t row = rowbase + cl.env;
-#ifndef CS_PROF_NO_SMALL
-                emit_legal<G>(legal, row, lg);
-                out_store(player + row, (uint8_t)p);
-#endif
-                if constexpr (G::ACTION_BYTES == 1) out_store((uint8_t*)out.action + row, (uint8_t)a);
-                else out_store((int16_t*)out.action + row, (int16_t)a);
-                g.step(a, m);
-                done = g.is_over();
-                if (done) {
-                    game_payoffs(g, r, m);
-                    if (out.final_obs) {   // Env.run's final state of every player (envs/env.py:161-164)
-#pragma unroll
-                        for (int q = 0; q < G::P; q++) {
-                            uint32_t fb[G::NB];
-                            g.observe(q, fb);
-                            write_obs_direct<G>((uint8_t*)out.final_obs + (row * G::P + q) * G::OBS, fb);
-                        }
-                    }
-                }
-#ifndef CS_PROF_NO_SMALL
-                if constexpr (!RewardPairs<G>::value) emit_reward<G>(reward, row, r);
-                out_store(done_o + row, (uint8_t)done);
-#endif
-                if constexpr (DQ == 0) {
-                    if (done) g.reset(m);
-                }
-            }
-#ifndef CS_PROF_NO_SMALL
-            if constexpr (RewardPairs<G>::value) {
-                if constexpr (RewardPairs<G>::mode == 2) emit_reward_t<G::EPW>(reward, rowbase, r, c);
-                else emit_reward_pairs(reward, rowbase, r, c);
-            }
-#endif
-            if constexpr (DQ > 0) {   // (the lockstep refill of the queues: below)
-                constexpr uint32_t CM = (1u << DqOf<G>::cb) - 1u;
-                if (__ballot(c.valid && done && (q.get(0) & CM) == 0u)) {
-                    if (c.valid && (q.get(0) & CM) < (uint32_t)DQ) dq_push(g, m, q);
-                }
-                if (c.valid && done) dq_reset(g, m, q);
-            }
-            refill<G>(m, cl.lane, flags & 1);
-            if (staged) restage<G>(m, stage[c.wid], cl.lane, c.valid);
-            continue;
-        }
-        // the policy counter's env id from scalars + the lane id at each step (a loop-invariant 64-bit value would be
-        // one more pair of VGPRs held across the step -- spilled, and its reload waits on the step's stores)
-        const uint64_t genv = A.env_base + (uint64_t)(c.wave_first + cl.lane);
-        const uint32_t pr = pol.at(seed, genv, t0 + (uint64_t)t, t == 0);
+        // each row stored where it is produced (round 5: the rows after the step's refill / restage loads ran 6-7 %
+        // slower on every torch allocation, profiles/EXPERIMENTS.md)
+        const uint32_t pr = pol.at(seed, genv0, t0 + (uint64_t)t, t == 0);
         int a;
         if constexpr (G::A <= 8) a = pick_legal_small<G::A>((uint32_t)lg, pr);
         else a = G::A <= 32 ? pick_legal32((uint32_t)lg, pr) : pick_legal(lg, pr);
-        constexpr int SK = SparseK<G>::value, SKW = (SK + 3) / 4;
-        uint32_t pos[SK];
-        uint32_t tail = 0;
-        if constexpr (SparseObs<G>::value) tail = g.observe_pos(p, pos);   // the pre-step view's one-hot positions
-        // with the stores after the step's loads, the view lives across the step, the refill and the restage: its
-        // positions (< 256) packed four per word, made opaque so the compiler keeps the packed form, not the array
-        uint32_t posw[SKW];
-        if constexpr (SparseObs<G>::value && SL) {
-            static_assert(G::OBS <= 256, "positions packed as bytes");
-#pragma unroll
-            for (int w = 0; w < SKW; w++) {
-                posw[w] = 0;
-#pragma unroll
-                for (int k = 4 * w; k < 4 * w + 4 && k < SK; k++) posw[w] |= pos[k] << (8 * (k - 4 * w));
-                asm volatile("" : "+v"(posw[w]));
-            }
+#if !CS_PROF_NO_OBS
+        if constexpr (SparseObs<G>::value) {
+            uint32_t pos[SparseK<G>::value];
+            const uint32_t tail = g.observe_pos(p, pos);
+            row_write_sparse<G::OBS, G::EPW, SparseK<G>::value, G::RAW_OBS>(
+                lds[c.wid], pos, obs + (rowbase + c.wave_first) * G::OBS, cl.lane, c.nvalid, !(flags & 4), tail);
+        } else {
+            emit_obs<G, G::EPW>(lds[c.wid], bits, obs, rowbase + c.wave_first, flags, cl);
         }
-        auto store_obs = [&]() {
-#ifndef CS_PROF_NO_OBS   // profiling builds only (tools: make variant DEFS=-DCS_PROF_NO_OBS): outputs incomplete
-            if constexpr (SparseObs<G>::value) {   // one-hot rows with a few known positions (row_write_sparse)
-                if constexpr (SL) {
-#pragma unroll
-                    for (int k = 0; k < SK; k++) pos[k] = (posw[k / 4] >> (8 * (k % 4))) & 255u;
-                }
-                row_write_sparse<G::OBS, G::EPW, SK, G::RAW_OBS>(
-                    lds[c.wid], pos, obs + (rowbase + c.wave_first) * G::OBS, cl.lane, c.nvalid, !(flags & 4), tail);
-            } else {
-                emit_obs<G, G::EPW>(lds[c.wid], bits, obs, rowbase + c.wave_first, flags, cl);
-            }
 #endif
-        };
-        if constexpr (!SL) store_obs();
         // the reward row starts from a zero the compiler cannot hoist out of the loop: a loop-invariant zero pair was
         // kept in a scratch spill whose reload, before each step's reward store, waited on vmcnt(0) -- on gfx950 every
         // store the wave had issued (the obs rows): a drain per step
         uint32_t zr = 0;
-#ifndef CS_ZERO_OPAQUE
-#define CS_ZERO_OPAQUE 1
-#endif
-        if constexpr (CS_ZERO_OPAQUE != 0) asm volatile("" : "+v"(zr));
+        asm volatile("" : "+v"(zr));
         float r[G::P];
 #pragma unroll
         for (int k = 0; k < G::P; k++) r[k] = __uint_as_float(zr);
         bool done = false;
-        const int64_t row = rowbase + cl.env;
-        // legal mask, player and action of the pre-step view, one word while they wait for the stores (A <= 16)
-        constexpr bool PACK_SMALL = SL && G::A <= 16 && G::ACTION_BYTES == 1;
-        uint32_t pre = 0;
-        if constexpr (PACK_SMALL) {
-            pre = (uint32_t)lg | (uint32_t)p << 16 | ((uint32_t)a & 255u) << 24;
-            asm volatile("" : "+v"(pre));
-        }
-        auto store_small_pre = [&]() {   // legal, player, action: the pre-step view and the action taken
-            const uint64_t lg_ = PACK_SMALL ? (uint64_t)(pre & 0xFFFFu) : lg;
-            const int p_ = PACK_SMALL ? (int)((pre >> 16) & 255u) : p;
-            const int a_ = PACK_SMALL ? (int)(int8_t)(pre >> 24) : a;
-#ifndef CS_PROF_NO_SMALL
-            emit_legal<G>(legal, row, lg_);
-            out_store(player + row, (uint8_t)p_);
-#endif
-            if constexpr (G::ACTION_BYTES == 1) out_store((uint8_t*)out.action + row, (uint8_t)a_);
-            else out_store((int16_t*)out.action + row, (int16_t)a_);
-        };
-        auto store_small_post = [&]() {   // reward, done: the transition's outcome
-#ifndef CS_PROF_NO_SMALL
-            if constexpr (!RewardPairs<G>::value) emit_reward<G>(reward, row, r);
-            out_store(done_o + row, (uint8_t)done);
-#endif
-        };
         if (c.valid) {
-            if constexpr (!SL) store_small_pre();
+            const int64_t row = rowbase + cl.env;
+#if !CS_PROF_NO_SMALL
+            emit_legal<G>(legal, row, lg);
+            out_store(player + row, (uint8_t)p);
+#endif
+            if constexpr (G::ACTION_BYTES == 1) out_store((uint8_t*)out.action + row, (uint8_t)a);
+            else out_store((int16_t*)out.action + row, (int16_t)a);
             g.step(a, m);
             done = g.is_over();
             if (done) {
@@ -821,20 +603,14 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
                     }
                 }
             }
-            if constexpr (!SL) store_small_post();
+#if !CS_PROF_NO_SMALL
+            emit_reward<G>(reward, row, r);
+            out_store(done_o + row, (uint8_t)done);
+#endif
             if constexpr (DQ == 0) {
                 if (done) g.reset(m);
             }
         }
-        auto store_reward_pairs = [&]() {
-#ifndef CS_PROF_NO_SMALL
-            if constexpr (RewardPairs<G>::value) {
-                if constexpr (RewardPairs<G>::mode == 2) emit_reward_t<G::EPW>(reward, rowbase, r, c);
-                else emit_reward_pairs(reward, rowbase, r, c);
-            }
-#endif
-        };
-        if constexpr (!SL) store_reward_pairs();
         if constexpr (DQ > 0) {
             // a lane ending its game with an empty queue makes every lane with room draw one deal ahead, in lockstep
             constexpr uint32_t CM = (1u << DqOf<G>::cb) - 1u;   // the header's count field
@@ -845,17 +621,6 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
         }
         refill<G>(m, cl.lane, flags & 1);
         if (staged) restage<G>(m, stage[c.wid], cl.lane, c.valid);
-        if constexpr (SL) {
-            // the step's rows leave after the step's loads (refill, restage): on gfx950 one counter (vmcnt) tracks
-            // loads and stores in issue order, so a load issued after the rows waits until every row store is
-            // acknowledged -- a drain whose length is the HBM write latency of the moment
-            store_obs();
-            if (c.valid) {
-                store_small_pre();
-                store_small_post();
-            }
-            store_reward_pairs();
-        }
     }
     bool keep = false;
     if constexpr (persist) {
@@ -866,7 +631,7 @@ __global__ __launch_bounds__(BLOCK, G::MIN_WAVES) void k_rollout(RolloutArgs arg
     }
     if (c.valid) {
         g.store(st, n, c.env);
-        if constexpr (DQ > 0 && !QHBM) {
+        if constexpr (DQ > 0) {
 #pragma unroll
             for (int w = 0; w < DQW; w++) st[(int64_t)(G::GW + w) * n + c.env] = q.get(w);
         }

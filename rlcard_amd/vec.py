@@ -235,12 +235,12 @@ class VecEnv:
     @property
     def rng_period(self):
         """Draws after which the stream position wraps (cs_game_info.rng_period): the byte ring of the lane-per-env
-        games holds CS_RING_SLOTS blocks (rlcard_amd/csrc/cs_ring.h), doudizhu's word layout 2."""
+        games holds RING_SLOTS_HOST blocks (rlcard_amd/csrc/cs_ring.h), doudizhu's word layout 2."""
         return int(self.info.rng_period)
 
     def _rng_geometry(self):
         """'words': doudizhu's two-block word window, or the Blackjack shoe's word stream (rng_period 624: one twist
-        per 624 draws); 'ring': the byte ring of the other lane-per-env games (rng_period = CS_RING_SLOTS x 624)."""
+        per 624 draws); 'ring': the byte ring of the other lane-per-env games (rng_period = RING_SLOTS_HOST x 624)."""
         if self.env_id == 'doudizhu':
             return 'ddz'
         return 'words' if self.rng_period == 624 else 'ring'

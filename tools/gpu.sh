@@ -12,6 +12,7 @@
 #   profile:GAME[:ARGS...]    kernel trace + stats, then FETCH_SIZE and WRITE_SIZE passes over bench.py
 #   ab:GAME:N:T:F1[:F2...]    tools/ab_rollout.py kernel-flag A/B (AB_PLAYERS / AB_WARM from the env)
 #   abl:GAME:N:T:LIB1[:LIB2]  the same rollout timed with several library builds (CARDSIM_LIB), interleaved runs
+#   abx:GAME:N:T:LIB1[:LIB2]  the same, all libraries in one process writing the same trajectory buffers
 #   devstate / listctr        device state (tools/device_state.py), rocprofv3 -L
 #   pmc:GAME:N:T:CTR...       one PMC pass over tools/ab_rollout.py
 #   ceiling                   plain read / write streams and torch fill_ on this box (tools/calib.py --ceiling)
@@ -77,6 +78,9 @@ for step in "$@"; do
     ab)
       run 400 "$O/ab_${a[1]}.log" python3 tools/ab_rollout.py "${a[1]}" "${a[2]}" "${a[3]}" "${a[@]:4}"
       cat "$O/ab_${a[1]}.log" ;;
+    abx)   # abx:GAME:N:T:LIB1[:LIB2..]  libraries A/B in ONE process over shared trajectory buffers (tools/ab_libs.py)
+      run 600 "$O/abx_${a[1]}.log" python3 tools/ab_libs.py "${a[1]}" "${a[2]}" "${a[3]}" "${a[@]:4}"
+      cat "$O/abx_${a[1]}.log" ;;
     abl)
       g=${a[1]}; n=${a[2]}; t=${a[3]}
       for rnd in 1 2 3; do
