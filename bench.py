@@ -97,6 +97,15 @@ def kernel_source_digest():
     return h.hexdigest()[:16]
 
 
+def product_library():
+    """The engine library this process loads, and whether it is the product build: rlcard_amd/libcardsim.so, which
+    the Makefile builds with no -D options (A/B and profiling variants are libcardsim_<name>.so, loaded through
+    CARDSIM_LIB). The kernel-source digest only identifies the product build's kernels, so a line measured on any other
+    library cites no traffic profile and says so."""
+    name = os.environ.get('CARDSIM_LIB', 'libcardsim.so')
+    return name, name == 'libcardsim.so'
+
+
 def measured_traffic(game, envs, T, kernel_ms=None):
     """HBM bytes per k_rollout launch of this configuration from the committed rocprofv3 profiles
     (profiles/traffic.json, written by tools/pmc_traffic.py), or None. An entry is one profile or a list of them
@@ -215,13 +224,14 @@ def main():
                     help='skip the CS_RNG_PHILOX phase (reported under "rng_philox")')
     ap.add_argument('--no-precondition', dest='precondition', action='store_false',
                     help='time from freshly seeded streams (optimistic: no MT block refills yet)')
-    ap.add_argument('--select', type=int, default=3,
-                    help='trajectory placement selection: allocate this many candidate trajectories, time the '
-                         'placement probe (cs_traj_probe) on each and run on the fastest (1: off); reported under '
-                         '"placement"')
-    ap.add_argument('--select-by', choices=('rollout', 'probe'), default='rollout',
-                    help='how --select ranks its candidates: one untimed rollout launch per candidate after the '
-                         'preconditioning (default; exact), or the placement probe before it (no env steps)')
+    ap.add_argument('--select', type=int, default=None,
+                    help='trajectory placement selection: allocate this many candidate trajectories and run on the '
+                         'fastest (1: off); default: what the library does, VecEnv.new_traj_out\'s '
+                         'PLACEMENT_CANDIDATES ranked by the placement probe; reported under "placement"')
+    ap.add_argument('--select-by', choices=('rollout', 'probe'), default='probe',
+                    help='how --select ranks its candidates: the placement probe before the preconditioning (default: '
+                         'the library\'s own choice, no env steps), or one untimed rollout launch per candidate after '
+                         'it (not what a library user gets)')
     ap.add_argument('--placement', type=int, default=3,
                     help='N=1: time a few launches into this many fresh trajectory allocations after the timed region '
                          '(untimed context under "placement"; 0: off)')
@@ -235,6 +245,7 @@ def main():
 
     import torch
     import torch.distributed as dist
+    from rlcard_amd import _abi
     from rlcard_amd.shard import ShardedVecEnv, rank_max, time_exchange, whole_job_rate
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -273,8 +284,8 @@ def main():
     N = args.envs or GAMES[game]['envs']
     env = ShardedVecEnv(game, N, rank, seed=42, device=local)   # global envs [rank*N, (rank+1)*N)
     env.reset()
-    by_rollout = args.select > 1 and args.select_by == 'rollout'
-    cands = [env.new_traj_out(T) for _ in range(args.select)] if by_rollout else None
+    by_rollout = (args.select or 0) > 1 and args.select_by == 'rollout'
+    cands = [env.new_traj_out(T, select=1) for _ in range(args.select)] if by_rollout else None
     traj = cands[0] if by_rollout else env.new_traj_out(T, select=args.select)
     probe_ms = list(getattr(env, 'placement_probe_ms', None) or []) if not by_rollout else []
 
@@ -359,7 +370,7 @@ def main():
     # the timed allocation's write ceiling (untimed): the placement probe writes the rollout's trajectory bytes (zeros,
     # the same tensors and order, no game logic), so its rate is what this allocation takes writes at
     write_probe = None
-    if args.select > 0:
+    if (args.select is None or args.select > 0) and hasattr(_abi.lib(), 'cs_traj_probe'):   # (old A/B builds lack it)
         wp_ms = sorted(env.probe_traj(traj, T) for _ in range(3))[1]
         wbytes = sum(traj[k].numel() * traj[k].element_size() for k in ('obs', 'legal', 'player', 'action', 'reward', 'done'))
         write_probe = dict(ms=wp_ms, bytes=wbytes, gbs=wbytes / (wp_ms * 1e-3) / 1e9, kernel_over_probe=kernel_ms / wp_ms,
@@ -373,7 +384,7 @@ def main():
         per = [kernel_ms]
         other_probe = []
         for _ in range(args.placement):
-            other = env.new_traj_out(T)
+            other = env.new_traj_out(T, select=1)
             other_probe.append(env.probe_traj(other, T))
             ms = []
             for k in range(4):
@@ -466,13 +477,22 @@ def main():
         }
         if write_probe is not None:
             line['roofline']['write_probe'] = write_probe
-        tr = measured_traffic(game, N, T, kernel_ms)
+        lib_name, is_product = product_library()
+        if not is_product:
+            line['non_product_build'] = lib_name
+        tr = measured_traffic(game, N, T, kernel_ms) if is_product else None
+        if not is_product:
+            line['roofline']['traffic_stale'] = 'non-product build %s: no traffic profile cited' % lib_name
         if tr is not None:   # per launch, like `achieved`; from the profile of this exact configuration and kernels
             if tr['stale']:
                 line['roofline']['traffic_stale'] = '%s measured other kernel sources' % tr['source']
             else:
                 line['roofline']['traffic'] = tr['bytes_per_launch']
                 line['roofline']['traffic_source'] = tr['source']
+                # the counter-based HBM rate beside `frac`: where the byte ring moves fewer bytes than the
+                # algorithmic count (traffic / alg < 1), this is the kernel's real share of the HBM peak
+                line['roofline']['traffic_over_alg'] = tr['bytes_per_launch'] / (B * N * T)
+                line['roofline']['traffic_frac'] = tr['bytes_per_launch'] / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
                 # the cited profile's own kernel time (rocprofv3 kernel trace of its timed launches) next to this
                 # line's HIP-event time: a profile is evidence for the line only if they agree
                 pk = tr.get('kernel_ns_timed_mean')
@@ -499,9 +519,10 @@ def main():
             else:
                 line['placement']['selection'] = dict(
                     candidates=len(probe_ms) or 1, by='probe', probe_ms=probe_ms or None,
-                    note='the timed trajectory is the fastest of the candidate allocations under the placement probe '
-                         '(cs_traj_probe: the rollout\'s writes, zeros, no game logic; DESIGN 7), chosen before '
-                         'warm-up')
+                    select_ms=getattr(env, 'placement_select_ms', None), library_default=args.select is None,
+                    note='the timed trajectory is VecEnv.new_traj_out\'s choice: the fastest of the candidate '
+                         'allocations under the placement probe (cs_traj_probe: the rollout\'s writes, zeros, no game '
+                         'logic; DESIGN.md placement), chosen before warm-up -- what a library user gets')
         line.update(gather_info)
         if philox_info is not None:
             line['rng_philox'] = philox_info

@@ -64,7 +64,13 @@ typedef struct {
     int32_t deal_queue_depth; /* DQ: deals the rollout may draw ahead (heads-up Limit / No-limit hold'em: 8 in this
                              build; 0 = no queue). state_words = game_words + 1 + 2 * DQ when DQ > 0; layout at
                              cs_get_env_state */
+    int32_t envs_per_wave; /* envs one 64-lane wave of cs_rollout plays (doudizhu 2, heads-up Limit / No-limit 32,
+                             otherwise 64): the write pattern cs_traj_probe reproduces */
 } cs_game_info;
+/* cs_game_info grows at its end between ABI versions (2: game_words, deal_queue_depth, envs_per_wave); a consumer
+ * built against this header checks cs_abi_version() >= CS_ABI_VERSION before calling cs_game_info_get, which writes
+ * sizeof(cs_game_info) bytes of this version. */
+#define CS_ABI_VERSION 2
 
 /* Outputs of reset/step/observe, all device pointers, one row per env:
  *   obs    uint8  [n][obs_dim]     the current player's observation (values 0/1; blackjack: the two scores;
@@ -313,6 +319,7 @@ int cs_debug_set_kernel_flags(cs_handle* h, int32_t flags);
 
 const char* cs_last_error(void);
 const char* cs_version(void);
+int32_t cs_abi_version(void);   /* CS_ABI_VERSION of the library */
 
 #ifdef __cplusplus
 }

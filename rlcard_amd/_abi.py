@@ -26,7 +26,10 @@ class GameInfo(C.Structure):
     _fields_ = [('obs_dim', C.c_int32), ('num_actions', C.c_int32), ('num_players', C.c_int32),
                 ('legal_bytes', C.c_int32), ('action_bytes', C.c_int32), ('state_words', C.c_int32),
                 ('action_feature_dim', C.c_int32), ('rng_period', C.c_int32), ('game_words', C.c_int32),
-                ('deal_queue_depth', C.c_int32)]
+                ('deal_queue_depth', C.c_int32), ('envs_per_wave', C.c_int32)]
+
+
+ABI_VERSION = 2   # include/cardsim.h CS_ABI_VERSION: the cs_game_info layout above
 
 
 class StepOut(C.Structure):
@@ -56,7 +59,7 @@ SYMBOLS = ('cs_game_info_get', 'cs_create', 'cs_destroy', 'cs_seed', 'cs_reset',
            'cs_load_env_rng', 'cs_get_rng_ctl', 'cs_cfr_train', 'cs_debug_holdem_rank7', 'cs_debug_ddz_legal',
            'cs_debug_set_serial_refill', 'cs_debug_set_kernel_flags',
            'cs_dmc_create', 'cs_dmc_destroy', 'cs_dmc_fill', 'cs_dmc_gather', 'cs_dmc_status', 'cs_dmc_layer1',
-           'cs_dmc_select', 'cs_last_error', 'cs_version')
+           'cs_dmc_select', 'cs_last_error', 'cs_version', 'cs_abi_version')
 
 _lib = None
 
@@ -111,8 +114,13 @@ def lib():
     L.cs_dmc_select.argtypes = [vp, vp, vp, vp, i64, C.c_float, u64, u64, u64, vp, vp]
     L.cs_last_error.restype = C.c_char_p
     L.cs_version.restype = C.c_char_p
+    if hasattr(L, 'cs_abi_version'):   # (older A/B builds lack it)
+        L.cs_abi_version.restype = C.c_int32
+        if L.cs_abi_version() < ABI_VERSION:
+            raise CardsimError('%s implements ABI version %d, this binding needs %d' % (LIB_PATH, L.cs_abi_version(),
+                                                                                     ABI_VERSION))
     for name in SYMBOLS:
-        if name not in ('cs_destroy', 'cs_dmc_destroy', 'cs_last_error', 'cs_version'):
+        if name not in ('cs_destroy', 'cs_dmc_destroy', 'cs_last_error', 'cs_version', 'cs_abi_version'):
             if name == 'cs_traj_probe' and not hasattr(L, name):   # older A/B builds (CARDSIM_LIB) lack it
                 continue
             getattr(L, name).restype = C.c_int

@@ -51,7 +51,8 @@ int set_device(const cs_handle* h)
 extern "C" {
 
 const char* cs_last_error(void) { return g_err.c_str(); }
-const char* cs_version(void) { return "rlcard_amd cardsim 0.1 (gfx950)"; }
+const char* cs_version(void) { return "rlcard_amd cardsim 0.2 (gfx950)"; }
+int32_t cs_abi_version(void) { return CS_ABI_VERSION; }
 
 int cs_game_info_get(int32_t game, const cs_config* cfg, cs_game_info* info)
 {
@@ -379,9 +380,7 @@ int cs_traj_probe(cs_handle* h, int32_t T, const cs_traj_out* out, void* stream)
         if (((uintptr_t)p & 15u) != 0) return fail(CS_E_INVALID, "trajectory tensors must be 16-byte aligned");
     int r = set_device(h);
     if (r != CS_OK) return r;
-    // envs per wave of the game's rollout kernel: DouDizhu two (k_rollout2), heads-up Limit / No-limit 32, else 64
-    const int32_t g = h->b.game, np = h->info.num_players;
-    const int32_t epw = g == CS_GAME_DOUDIZHU ? 2 : ((g == CS_GAME_LIMIT || g == CS_GAME_NOLIMIT) && np == 2 ? 32 : 64);
+    const int32_t epw = h->info.envs_per_wave;   // the game's rollout kernel's (G::EPW, filled by game_info)
     hipError_t e = cs::launch_traj_probe(h->b, T, *out, h->info.obs_dim, h->info.legal_bytes, h->info.action_bytes, epw,
                                          (hipStream_t)stream);
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_traj_probe");

@@ -406,6 +406,7 @@ int bjs_game_info(const cs_config* cfg, cs_game_info* info)
     info->action_feature_dim = 2;
     info->rng_period = MT_N;   // position = words consumed of the current 624-word block
     info->game_words = bjs::WORDS;
+    info->envs_per_wave = WAVE;   // k_rollout: one lane per env
     return CS_OK;
 }
 

@@ -777,7 +777,7 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint32_t* st, int64_t n
 #define CS_DDZ_PAIR_WAVES 4   // waves per block (the group table in LDS is shared by 2 x this many envs)
 #endif
 #ifndef CS_DDZ_PAIR_MINW
-#define CS_DDZ_PAIR_MINW 5    // waves per SIMD the registers must allow
+#define CS_DDZ_PAIR_MINW 6    // waves per SIMD the registers must allow (80 VGPRs; 5: +1 %, 4: +13 %, EXPERIMENTS R6-1)
 #endif
 constexpr int HW = WAVE / 2;                         // lanes per env
 constexpr int PWPB = CS_DDZ_PAIR_WAVES, PBLOCK = PWPB * WAVE;
@@ -834,13 +834,15 @@ struct PEnv {
     {
         return keep64(p == 0, h0) | keep64(p == 1, h1) | keep64(p == 2, h2);
     }
-    // Env::apply_with for the half's env (hl: lane in the half; q: its played cards)
-    __device__ __forceinline__ void apply_with(uint32_t a, uint64_t c, uint32_t gid, int hl, uint64_t* q)
+    // Env::apply_with for the half's env (lane: the caller's lane id, hl: lane in the half; q: its played cards)
+    __device__ __forceinline__ void apply_with(uint32_t a, uint64_t c, uint32_t gid, int lane, int hl, uint64_t* q)
     {
         const uint32_t p = cur();
-        const uint64_t down = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)hcnt, 1) |
-                              ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(hcnt >> 32), 1) << 32);
-        const uint32_t hdown = (uint32_t)__shfl_down((int)hid, 1);
+        // the trace shifted down one lane (lanes 3..10 read their upper neighbour, inside the half)
+        const int src = ((lane & HW) + ((hl + 1) & (HW - 1))) << 2;
+        const uint64_t down = (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)hcnt) |
+                              ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(hcnt >> 32)) << 32);
+        const uint32_t hdown = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)hid);
         const bool mid = hl >= 3 && hl < 11;
         hcnt = hl == 11 ? c : (mid ? down : 0ull);
         hid = hl == 11 ? a : (mid ? hdown : NO_ACTION);
@@ -1378,6 +1380,7 @@ void k_rollout2(PairArgs args)
         int lane_o = lane;
         asm volatile("" : "+v"(lane_o));
         const int lane = lane_o, hl = lane & (HW - 1);
+        PairLds& L = lds[wid][lane >> 5];   // (from the opaque lane: its member addresses are not held across steps)
         const PairArgs& A = arg();
         const Tab& tb = A.tb;
         const cs_traj_out& out = A.out;
@@ -1441,7 +1444,7 @@ void k_rollout2(PairArgs args)
         write_rows2(L, valid && !(CS_PROF_DDZ & 2) ? (uint8_t*)out.obs + row * OBS : nullptr,
                     valid && !ovf && !(CS_PROF_DDZ & 1) ? lrow : nullptr, zw, lane);
         const uint32_t p = e.cur();
-        if (valid) e.apply_with(a, ca, ga, hl, L.q);
+        if (valid) e.apply_with(a, ca, ga, lane, hl, L.q);
         const bool done = valid && e.over();
         if (valid && hl == 0) {
             ((uint8_t*)out.player)[row] = (uint8_t)p;

@@ -67,6 +67,7 @@ int game_info(int32_t game, const cs_config* cfg, cs_game_info* info)
         info->action_feature_dim = 54;
         info->rng_period = 2 * 624;
         info->game_words = ddz::WORDS;
+        info->envs_per_wave = 2;   // k_rollout2: one env per half-wave
         return CS_OK;
     default:
         return CS_E_UNSUPPORTED;

@@ -701,6 +701,7 @@ static void fill_info(cs_game_info* info)
     info->rng_period = (int32_t)RING;
     info->deal_queue_depth = DqOf<G>::value;
     info->game_words = G::WORDS - DqOf<G>::words;
+    info->envs_per_wave = G::EPW;
 }
 
 template <class G>

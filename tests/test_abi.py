@@ -27,10 +27,16 @@ def test_library_exports_every_declared_symbol():
 def test_game_info_shapes():
     shapes = {'leduc-holdem': (36, 4, 2, 1, 1), 'limit-holdem': (72, 4, 2, 1, 1), 'blackjack': (2, 2, 1, 1, 1),
               'doudizhu': (901, 27472, 3, 3434, 2), 'no-limit-holdem': (54, 5, 2, 1, 1)}
+    epw = {'leduc-holdem': 64, 'limit-holdem': 32, 'blackjack': 64, 'doudizhu': 2, 'no-limit-holdem': 32}
     for game, (o, a, p, lb, ab) in shapes.items():
         info, _ = _abi.game_info(game)
         assert (info.obs_dim, info.num_actions, info.num_players, info.legal_bytes, info.action_bytes) == \
             (o, a, p, lb, ab)
+        assert info.envs_per_wave == epw[game], game   # cs_traj_probe's write pattern
+    for game, n in (('limit-holdem', 5), ('no-limit-holdem', 12), ('leduc-holdem', 4)):
+        assert _abi.game_info(game, n)[0].envs_per_wave == 64
+    assert _abi.game_info('blackjack', 6, 8)[0].envs_per_wave == 64
+    assert _abi.lib().cs_abi_version() == _abi.ABI_VERSION == 2
 
 
 def test_doudizhu_action_table_is_compiled_in():

@@ -13,7 +13,7 @@ GAMES = [('leduc-holdem', 1000, 8), ('limit-holdem', 700, 6), ('doudizhu', 37, 4
 
 def _guarded(v, T):
     """the trajectory tensors carved from one buffer with 4 KiB guard bands of 0xA5 between and around them"""
-    like = v.new_traj_out(T)
+    like = v.new_traj_out(T, select=1)
     g = 4096
     sizes = {k: x.numel() * x.element_size() for k, x in like.items()}
     total = g + sum((s + 15) // 16 * 16 + g for s in sizes.values())
@@ -58,3 +58,33 @@ def test_probe_and_selection_leave_the_envs_alone(game, n, T):
         torch.cuda.synchronize()
         for key in ra:
             assert torch.equal(ra[key], rb[key]), (game, key)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('game,n,T', [('leduc-holdem', 1 << 20, 256), ('doudizhu', 65536, 64)])
+def test_default_placement_is_within_5pct_of_the_fastest(game, n, T):
+    """VecEnv.new_traj_out's default choice ranks candidate allocations by the write-only probe. Ground truth is the
+    rollout itself: four candidate trajectories (BASELINE shapes) alive at once, each timed by rollout launches in the
+    same process after a short warm-up; the allocation the probe ranks first must run within 5 % of the fastest
+    candidate (the probe separates the 20-25 % placement classes; within a class it cannot rank)."""
+    v = VecEnv(game, n, seed=42, device=0)
+    v.reset()
+    cands = [v.new_traj_out(T, select=1) for _ in range(4)]
+    t = 0
+    for _ in range(8):
+        v.rollout(T, 5, t * T, out=cands[t % 4])
+        t += 1
+    probe = [min(v.probe_traj(c, T) for _ in range(2)) for c in cands]
+    roll = [[] for _ in cands]
+    for _ in range(3):
+        for i, c in enumerate(cands):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            v.rollout(T, 5, t * T, out=c)
+            e1.record()
+            t += 1
+            torch.cuda.synchronize()
+            roll[i].append(e0.elapsed_time(e1))
+    best = [sorted(r)[1] for r in roll]
+    pick = min(range(len(cands)), key=lambda i: probe[i])
+    assert best[pick] <= 1.05 * min(best), (game, probe, best)

@@ -25,9 +25,9 @@ for i in range(inst):
     v.reset()
     Tv = {f: (f if Ts else T) for f in variants}
     # one allocation of the largest T; smaller T launches write its leading steps (same buffers, no allocation effect)
-    big = v.new_traj_out(max(Tv.values())) if Ts else None
+    big = v.new_traj_out(max(Tv.values()), select=1) if Ts else None
     trs = {f: {k: x[:Tv[f]] for k, x in big.items()} for f in variants} if Ts else None
-    tr = v.new_traj_out(T) if not Ts else trs[variants[0]]
+    tr = v.new_traj_out(T, select=1) if not Ts else trs[variants[0]]
     t = 0   # absolute step of the policy stream
     for _ in range(int(os.environ.get('AB_WARM', '40'))):
         v.rollout(Tv[variants[0]], 5, t, out=tr); t += Tv[variants[0]]

@@ -65,6 +65,10 @@ int main(int argc, char** argv)
         keys[2 * i + 1] = b;
         klen[i] = l;
     }
+    if (cs_abi_version() < CS_ABI_VERSION) {   /* cs_game_info of this header's size (include/cardsim.h) */
+        fprintf(stderr, "library ABI %d < header ABI %d\n", (int)cs_abi_version(), CS_ABI_VERSION);
+        return 2;
+    }
     cs_config cfg;
     memset(&cfg, 0, sizeof(cfg));
     cfg.num_decks = -1;

@@ -14,7 +14,7 @@ inst = int(sys.argv[4]) if len(sys.argv) > 4 else 4
 for i in range(inst):
     v = VecEnv(game, n, seed=42 + i, device=0)
     v.reset()
-    tr = v.new_traj_out(T)
+    tr = v.new_traj_out(T, select=1)
     for t in range(int(os.environ.get('AB_WARM', '30'))):
         v.rollout(T, 5, t * T, out=tr)
     torch.cuda.synchronize()

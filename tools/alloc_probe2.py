@@ -70,7 +70,7 @@ for i in range(inst):
     bufs, keep = {}, []
     for name in order:   # allocated in this order
         if name == 'torch':
-            bufs[name] = v.new_traj_out(T)
+            bufs[name] = v.new_traj_out(T, select=1)
         else:
             bufs[name], k = raw_traj(v, T, 0x4 if name == 'contiguous' else 0x0)
             keep += k

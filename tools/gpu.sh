@@ -81,6 +81,9 @@ for step in "$@"; do
     abx)   # abx:GAME:N:T:LIB1[:LIB2..]  libraries A/B in ONE process over shared trajectory buffers (tools/ab_libs.py)
       run 600 "$O/abx_${a[1]}.log" python3 tools/ab_libs.py "${a[1]}" "${a[2]}" "${a[3]}" "${a[@]:4}"
       cat "$O/abx_${a[1]}.log" ;;
+    pdef)   # pdef:GAME:N:T:K  default (probe-selected) vs unselected trajectory placements (tools/placement_default.py)
+      run 400 "$O/pdef_${a[1]}.jsonl" python3 tools/placement_default.py "${a[1]}" "${a[2]}" "${a[3]}" "${a[4]}"
+      tail -1 "$O/pdef_${a[1]}.jsonl" ;;
     abl)
       g=${a[1]}; n=${a[2]}; t=${a[3]}
       for rnd in 1 2 3; do

@@ -27,7 +27,7 @@ def main():
     lib.wpat_run.argtypes = [C.POINTER(WArgs), C.c_int, C.c_void_p]
     v = VecEnv(game, n, seed=42, device=0)
     v.reset()
-    trajs = [v.new_traj_out(T) for _ in range(K)]
+    trajs = [v.new_traj_out(T, select=1) for _ in range(K)]
     stream = torch.cuda.current_stream()
     t = 0
     for _ in range(bench.precondition_launches(game, T, v)):

@@ -28,7 +28,7 @@ def make_env():
 
 
 envs = [make_env() for _ in range(K if mode in ('env', 'both') else 1)]
-trajs = [envs[0].new_traj_out(T) for _ in range(K if mode in ('traj', 'both') else 1)]
+trajs = [envs[0].new_traj_out(T, select=1) for _ in range(K if mode in ('traj', 'both') else 1)]
 pairs = [(envs[i if len(envs) > 1 else 0], trajs[i if len(trajs) > 1 else 0]) for i in range(K)]
 pre = bench.precondition_launches(game, T, envs[0])
 t = {id(v): 0 for v in envs}

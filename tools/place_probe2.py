@@ -19,7 +19,7 @@ g = bench.GAMES[game]
 n, T = g['envs'], g['T']
 v = VecEnv(game, n, seed=42, device=0)
 v.reset()
-base = v.new_traj_out(T)
+base = v.new_traj_out(T, select=1)
 
 
 SKEW = 352 << 10   # skew mode: tensor k starts k x 352 KiB past a 2 MiB boundary (spread over the 2 MiB page)
@@ -47,7 +47,7 @@ for i in range(1, K):
     if what == 'alt':    # alternate unskewed / skewed single allocations
         variants.append(carve(base, SKEW if i % 2 else 0))
         continue
-    fresh = v.new_traj_out(T)
+    fresh = v.new_traj_out(T, select=1)
     d = dict(base)
     keys = {'obs': ['obs'], 'reward': ['reward'], 'small': ['legal', 'player', 'action', 'done']}[what]
     for k in keys:

@@ -26,7 +26,7 @@ class _Dev:
 def contiguous_traj(v, T, hip, keep):
     """the trajectory tensors of new_traj_out, each in its own physically contiguous allocation"""
     out = {}
-    for k, x in v.new_traj_out(T).items():
+    for k, x in v.new_traj_out(T, select=1).items():
         nbytes = x.numel() * x.element_size()
         p = C.c_void_p()
         assert hip.hipExtMallocWithFlags(C.byref(p), nbytes, 0x4) == 0, 'hipExtMallocWithFlags'
@@ -57,7 +57,7 @@ def main():
             tr['legal'] = torch.empty((T, n, pad[0]), dtype=torch.uint8, device=0)
             tr['obs'] = torch.empty((T, n, pad[1]), dtype=torch.uint8, device=0)
         return tr
-    trajs = [('torch%d' % i, padded(v.new_traj_out(T))) for i in range(K)]
+    trajs = [('torch%d' % i, padded(v.new_traj_out(T, select=1))) for i in range(K)]
     trajs += [('contig%d' % i, contiguous_traj(v, T, hip, keep)) for i in range(Cn if not pad else 0)]
     t = 0
     for _ in range(bench.precondition_launches(game, T, v)):

@@ -24,7 +24,7 @@ keep = []   # AP_KEEP=1: keep every instance alive (each new one lands on other 
 for i in range(inst):
     v = VecEnv(game, n, seed=42, device=0)
     v.reset()
-    tr = v.new_traj_out(T)
+    tr = v.new_traj_out(T, select=1)
     pre = bench.precondition_launches(game, T, v)
     for c in range(pre):
         v.rollout(T, 5, c * T, out=tr)

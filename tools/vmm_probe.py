@@ -110,13 +110,13 @@ def main():
     rng = random.Random(7)
     v = VecEnv(game, n, seed=42, device=0)
     v.reset()
-    like = v.new_traj_out(T)
+    like = v.new_traj_out(T, select=1)
     keep = []
     trajs = []
     kinds = os.environ.get('VMM_KINDS', 'torch,vmm_shuf,vmm_id,torch,vmm_shuf,vmm_id,torch,contig').split(',')
     for i, kind in enumerate(kinds):
         if kind == 'torch':
-            tr = v.new_traj_out(T)
+            tr = v.new_traj_out(T, select=1)
         elif kind == 'contig':
             tr, p = contig_traj(h, like)
             keep.append(p)
