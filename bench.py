@@ -288,6 +288,7 @@ def main():
     cands = [env.new_traj_out(T, select=1) for _ in range(args.select)] if by_rollout else None
     traj = cands[0] if by_rollout else env.new_traj_out(T, select=args.select)
     probe_ms = list(getattr(env, 'placement_probe_ms', None) or []) if not by_rollout else []
+    select_ms = getattr(env, 'placement_select_ms', None) if not by_rollout else None
 
     stream = torch.cuda.current_stream()
     t_launch = 0
@@ -519,7 +520,7 @@ def main():
             else:
                 line['placement']['selection'] = dict(
                     candidates=len(probe_ms) or 1, by='probe', probe_ms=probe_ms or None,
-                    select_ms=getattr(env, 'placement_select_ms', None), library_default=args.select is None,
+                    select_ms=select_ms, library_default=args.select is None,
                     note='the timed trajectory is VecEnv.new_traj_out\'s choice: the fastest of the candidate '
                          'allocations under the placement probe (cs_traj_probe: the rollout\'s writes, zeros, no game '
                          'logic; DESIGN.md placement), chosen before warm-up -- what a library user gets')
