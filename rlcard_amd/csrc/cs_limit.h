@@ -176,7 +176,7 @@ __device__ __forceinline__ void holdem_deal2(Rng& rng, uint32_t& holes, uint32_t
 #endif
     if (!staged) {
 #pragma unroll
-        for (int k = 0; k < 9; k++) js[k] = rng.interval(51u - (uint32_t)k);
+        for (int k = 0; k < 9; k++) js[k] = rng.interval_loop(51u - (uint32_t)k);
     }
     uint32_t d0 = 0, d1 = 0;
 #if !CS_PROF_NO_TRACK

@@ -257,6 +257,39 @@ struct RingLane {
         mask |= mask >> 1;
         mask |= mask >> 2;
         mask |= mask >> 4;
+        if (__builtin_constant_p(max) && max == mask) return next8() & mask;   // e.g. randint(0, 2): never rejects
+        if constexpr (MODE == STAGE_LDS) {
+            // the next four staged bytes at once: per byte t = b & mask, (t | 0x80) - (max + 1) has bit 7 set exactly
+            // when t > max (no borrow between bytes for max < 128); the first accepted byte is the draw. The loop
+            // below only runs past four rejections in a row (~0.1 % of a 52-card deal) or at the staged row's end.
+            // The second dword may reach into the row's pad (PAD >= 4), its bytes past sn unused.
+            const uint32_t k0 = staged_offset();
+            if (max < 128u && k0 + 4u <= sn) {
+                const uint32_t* row = (const uint32_t*)(stg + (k0 & ~3u));
+                const uint32_t x = __builtin_amdgcn_alignbyte(row[1], row[0], k0 & 3u) & (mask * 0x01010101u);
+                const uint32_t acc = ~((x | 0x80808080u) - (max + 1u) * 0x01010101u) & 0x80808080u;
+                if (acc) {
+                    const uint32_t b = (uint32_t)__builtin_ctz(acc) >> 3;
+                    advance_by(b + 1u);
+                    return (x >> (8u * b)) & 255u;
+                }
+                advance_by(4u);
+            }
+        }
+        return interval_loop(max, mask);
+    }
+    // the same draw one byte at a time (cold paths: keeps the kernels' code small)
+    __device__ __forceinline__ uint32_t interval_loop(uint32_t max)
+    {
+        if (max == 0) return 0;
+        uint32_t mask = max;
+        mask |= mask >> 1;
+        mask |= mask >> 2;
+        mask |= mask >> 4;
+        return interval_loop(max, mask);
+    }
+    __device__ __forceinline__ uint32_t interval_loop(uint32_t max, uint32_t mask)
+    {
         uint32_t v;
         do {
             v = next8() & mask;
@@ -277,7 +310,7 @@ struct RingLane {
     // random_interval(i) for i = hi .. 1 with every result discarded: only how many bytes the draws consume matters.
     // The staged bytes are read as whole dwords at any byte offset (alignbyte of two aligned dwords) and scanned
     // branch-free -- per byte: the mask width of i, a bit-field extract, one compare -- for the draws i = hi .. 2; the
-    // last draw (mask 1) always takes exactly one byte. A lane that runs out of staged bytes finishes through interval().
+    // last draw (mask 1) always takes exactly one byte. A lane that runs out of staged bytes finishes through interval_loop().
     __device__ __forceinline__ void skip_intervals(uint32_t hi)
     {
         uint32_t i = hi;
@@ -314,11 +347,11 @@ struct RingLane {
                 advance_by(cnt);
             }
         }
-        for (; i >= 1; i--) (void)interval(i);
+        for (; i >= 1; i--) (void)interval_loop(i);
     }
 
     // random_interval(i) for i = hi, hi - 1, .., 1 in stream order, put(k, value of draw k): one branch-free pass over
-    // the staged bytes (per byte: extract under the mask of the current i, accept, count), interval() past their end
+    // the staged bytes (per byte: extract under the mask of the current i, accept, count), interval_loop() past their end
     template <class F>
     __device__ __forceinline__ void draw_intervals(uint32_t hi, F&& put)
     {
@@ -346,7 +379,7 @@ struct RingLane {
                 advance_by(cnt);
             }
         }
-        for (; i >= 1; i--) put(hi - i, interval(i));
+        for (; i >= 1; i--) put(hi - i, interval_loop(i));
     }
 };
 

@@ -207,6 +207,8 @@ struct StageBytesOf<W, PAD, ROWS, true> {
 template <class G>
 struct StageBytes {
     static constexpr int value = StageBytesOf<G::STAGE_W, G::STAGE_PAD, G::EPW, G::STAGE_MODE == STAGE_LDS>::value;
+    // the staged-byte scans read one dword past their last staged byte (RingLane::interval, draw_intervals)
+    static_assert(G::STAGE_MODE != STAGE_LDS || G::STAGE_PAD >= 4, "stage rows need a pad of at least a dword");
 };
 // batch restage threshold (ring_restage_wave): the game's STAGE_RF, else its STAGE_R (restage exactly the needy lanes)
 template <class G, class = void>
