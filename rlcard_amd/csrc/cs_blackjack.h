@@ -10,21 +10,19 @@
 //   rlcard/games/blackjack/game.py:160-205  state: own hand; dealer hand[1:] until the game is over; is_over
 //   rlcard/games/blackjack/judger.py:2-73   scores with soft aces; winner codes 2 / 1 / -1
 //   rlcard/envs/blackjack.py:38-103         obs = [score(own), score(dealer visible)], legal {hit, stand}, payoff 1/0/-1
-// The shuffle is not applied to a deck in memory (51 dependent LDS byte swaps per game were the kernel's critical
-// path): its draws are kept, and the card at a final deck position is found by undoing the swaps from the last one
-// back -- only the ~6 positions a game deals are ever looked up. The draws live in registers (13 words); the deal of
-// init_game first draws all of its 2 (P + 1) positions (they depend on the stream and the removed set only) and then
-// traces them back together, four positions per word (SWAR byte compares, ~3 ops per position and swap instead of 5).
-// "deck.pop(idx)" is an order-statistic removal: a 52-bit removed mask over the shuffled positions; the idx-th
-// remaining card is the idx-th clear bit.
+// The shuffle is applied once per game, in the reset's pass over the staged stream bytes: each accepted draw swaps two
+// bytes of the identity deck laid out in the lane's LDS scratch (in-order LDS: a swap waits only for its own two
+// loads), and the shuffled deck then lives in registers (13 words). A dealt position's card is a select over those
+// words (~18 VALU; undoing the 51 swaps per card instead cost ~270). "deck.pop(idx)" is an order-statistic removal: a
+// 52-bit removed mask over the shuffled positions; the idx-th remaining card is the idx-th clear bit.
 // Packed state, 32 u32 words per env (word-major [32][N]):
-//   0..12  the shuffle's draws: byte k = j of Fisher-Yates swap k (positions 51 - k and j); card id = sorted position
+//   0..12  the shuffled deck: byte p = card id (sorted-deck index) at position p
 //   13     removed mask bits 0..31;  14: removed bits 32..51 | deck_len << 20 | game_pointer << 26 | over << 29
 //   15..29 hands: hand h (players 0..P-1, dealer = P) bytes 12h .. 12h+11 (words past 15 + 3 (P + 1) stay zero)
 //   30     hand sizes 4 bits each (5 hands) | winner codes 2 bits per player << 20 (0 none, 1 tie, 2 win, 3 loss)
 // Inside a kernel words 0..12 are registers; 13, 14, 30 and the hands a per-lane LDS scratch (lane-interleaved, so
 // uniform word indices are bank-conflict free; the hands are indexed dynamically), which the reset's draw pass also
-// uses to collect the 51 draws (per-lane byte positions) before they move to registers.
+// uses to shuffle the deck (per-lane byte positions) before it moves to registers.
 #pragma once
 #include "cs_device.h"
 #include "cs_prof.h"
@@ -39,7 +37,7 @@ struct Blackjack {
     static constexpr bool RAW_OBS = true;      // observe() returns byte values, not a 0/1 bitmap
     static constexpr int HAND_CAP = 12;
     static constexpr int HAND_W = 3 * (NP + 1);                 // state words 15.. the hands use
-    static constexpr int SCRATCH_WORDS = 3 + HAND_W > 13 ? 3 + HAND_W : 13;   // >= 13: the reset's draw bytes
+    static constexpr int SCRATCH_WORDS = 3 + HAND_W > 13 ? 3 + HAND_W : 13;   // >= 13: the reset's deck bytes
     // MT staging (see MtLaneT)
     // MT staging rows of 128 bytes: the reset's ~57 draws come out of one branch-free pass over them
     // (RingLane::draw_intervals); measured 17.2 ms per 2^20 x 64 launch vs 19.9 with 64-byte rows (3 waves per SIMD
@@ -52,7 +50,7 @@ struct Blackjack {
 
     uint32_t* s;       // lane scratch: word i at s[i * WAVE]: 0 = state word 13, 1 = 14, 2 = 30, 3 + q = 15 + q
     int infinite;
-    uint32_t jw[13];   // state words 0..12: the shuffle's draws
+    uint32_t jw[13];   // state words 0..12: the shuffled deck, byte p = the card at position p
     // running judge totals (registers, rebuilt from the hands by load()): hand h's card values with aces as 11 |
     // its aces << 8; [NP + 1] the same over the dealer's cards after the first (the visible dealer score)
     uint32_t tot[NP + 2];
@@ -182,48 +180,19 @@ struct Blackjack {
         }
         return base;
     }
-    // the card at final deck position x: undo the swaps from the last (i = 1) to the first (i = 51)
+    // the card at deck position x: byte x & 3 of word x >> 2, the word picked by a select tree on the bits of x >> 2
+    // (bitwise selects, v_bfi_b32: as ?: on an array the compiler turns the tree into a dynamically indexed stack copy)
     __device__ __forceinline__ int card_at(int x) const
     {
-#if CS_PROF_BJ_NOTRACE   // profiling builds only (cs_prof.h)
-        return x;
-#endif
-        // the draws pass through an empty asm: opaque values, so the compiler cannot hoist the 51 extracted draws out
-        // of the dealer's loop into 51 live registers (occupancy)
-        uint32_t w[13];
-#pragma unroll
-        for (int q = 0; q < 13; q++) {
-            w[q] = jw[q];
-            asm volatile("" : "+v"(w[q]));
-        }
-#pragma unroll
-        for (int i = 1; i <= 51; i++) {
-            const int k = 51 - i;
-            const int j = (int)__builtin_amdgcn_ubfe(w[k >> 2], 8 * (k & 3), 6);
-            x = x == i ? j : (x == j ? i : x);
-        }
-        return x;
-    }
-    // card_at for four positions per word (bytes; unused bytes 63 never match): undoing swap (i, j) flips a byte
-    // x in {i, j} by i ^ j. Bytes are < 64, so (b + 0x7F) sets bit 7 exactly when b != 0, without carries.
-    template <int NW>
-    __device__ __forceinline__ void cards_at(uint32_t (&X)[NW]) const
-    {
-#if CS_PROF_BJ_NOTRACE
-        return;
-#endif
-#pragma unroll
-        for (int i = 1; i <= 51; i++) {
-            const int k = 51 - i;
-            const uint32_t J = __builtin_amdgcn_perm(0u, jw[k >> 2], (uint32_t)(k & 3) * 0x01010101u);   // j x 4
-            const uint32_t I = (uint32_t)i * 0x01010101u, D = I ^ J;
-#pragma unroll
-            for (int w = 0; w < NW; w++) {
-                const uint32_t both = ((X[w] ^ I) + 0x7F7F7F7Fu) & ((X[w] ^ J) + 0x7F7F7F7Fu);
-                const uint32_t m = ~both & 0x80808080u;
-                X[w] ^= D & (m - (m >> 7));
-            }
-        }
+        const uint32_t w = (uint32_t)x >> 2;
+        const uint32_t m0 = 0u - (w & 1u), m1 = 0u - ((w >> 1) & 1u), m2 = 0u - ((w >> 2) & 1u), m3 = 0u - (w >> 3);
+        const auto sel = [](uint32_t m, uint32_t hi, uint32_t lo) { return (hi & m) | (lo & ~m); };
+        const uint32_t a0 = sel(m0, jw[1], jw[0]), a1 = sel(m0, jw[3], jw[2]), a2 = sel(m0, jw[5], jw[4]);
+        const uint32_t a3 = sel(m0, jw[7], jw[6]), a4 = sel(m0, jw[9], jw[8]), a5 = sel(m0, jw[11], jw[10]);
+        const uint32_t b0 = sel(m1, a1, a0), b1 = sel(m1, a3, a2), b2 = sel(m1, a5, a4);
+        const uint32_t c0 = sel(m2, b1, b0), c1 = sel(m2, jw[12], b2);
+        const uint32_t d = sel(m3, c1, c0);
+        return (int)__builtin_amdgcn_ubfe(d, 8u * ((uint32_t)x & 3u), 8u);
     }
 
     // Dealer.deal_card's draw: idx = choice(len(deck)), the idx-th remaining position; deck.pop(idx) unless infinite
@@ -271,28 +240,27 @@ struct Blackjack {
     template <class Rng>
     __device__ __forceinline__ void reset(Rng& rng)
     {
-        // 52-card Fisher-Yates (i = 51..1, j = randint(0, i + 1)): its draws, byte k of scratch words 0..12 (LDS byte
-        // stores at per-lane positions), then into registers; then the initial deal (game.py:22-54): two rounds of
-        // players 0..P-1 and the dealer
-        uint8_t* jb = (uint8_t*)s;
-        rng.draw_intervals(51u, [&](uint32_t k, uint32_t j) { jb[(k >> 2) * (WAVE * 4) + (k & 3u)] = (uint8_t)j; });
+        // 52-card Fisher-Yates (i = 51..1, j = randint(0, i + 1); dealer.py:4-37) on the identity deck in scratch words
+        // 0..12 (byte p of the lane's deck at (p >> 2) * WAVE words + p & 3), each accepted draw swapping positions i
+        // and j where the draw pass finds it; then the deck into registers, and the initial deal (game.py:22-54): two
+        // rounds of players 0..P-1 and the dealer
+#pragma unroll
+        for (int w = 0; w < 13; w++) L(w) = 0x03020100u + 0x04040404u * (uint32_t)w;
+        uint8_t* deck = (uint8_t*)s;
+        rng.draw_intervals(51u, [&](uint32_t k, uint32_t j) {
+            const uint32_t i = 51u - k;
+            uint8_t* pi = deck + (i >> 2) * (WAVE * 4) + (i & 3u);
+            uint8_t* pj = deck + (j >> 2) * (WAVE * 4) + (j & 3u);
+            const uint8_t ci = *pi, cj = *pj;
+            *pi = cj;
+            *pj = ci;
+        });
 #pragma unroll
         for (int w = 0; w < 13; w++) jw[w] = L(w);
-        jw[12] &= 0xFFFFFFu;   // byte 51: no draw
         clear_table();
-        // every dealt position first (they depend only on the stream and the removed set), traced back together
-        constexpr int ND = 2 * (NP + 1), NW = (ND + 3) / 4;
-        uint32_t X[NW];
+        constexpr int ND = 2 * (NP + 1);
 #pragma unroll
-        for (int w = 0; w < NW; w++) X[w] = 0x3F3F3F3Fu;
-#pragma unroll
-        for (int d = 0; d < ND; d++) {
-            const uint32_t sh = 8u * (uint32_t)(d & 3);
-            X[d >> 2] = (X[d >> 2] & ~(255u << sh)) | (uint32_t)deal_pos(rng) << sh;
-        }
-        cards_at(X);
-#pragma unroll
-        for (int d = 0; d < ND; d++) add_card(d % (NP + 1), (int)((X[d >> 2] >> (8 * (d & 3))) & 255u));
+        for (int d = 0; d < ND; d++) add_card(d % (NP + 1), card_at(deal_pos(rng)));
     }
 
     template <class Rng>

@@ -26,9 +26,6 @@
 #ifndef CS_PROF_NO_SKIP
 #define CS_PROF_NO_SKIP 0      // Limit / No-limit: no skip scan of the 42 undealt draws
 #endif
-#ifndef CS_PROF_BJ_NOTRACE
-#define CS_PROF_BJ_NOTRACE 0   // Blackjack: no swap trace-back (a dealt position is its card)
-#endif
 #ifndef CS_PROF_DDZ
 #define CS_PROF_DDZ 0          // DouDizhu k_rollout2: bit 0 no legal rows, bit 1 no obs rows
 #endif
