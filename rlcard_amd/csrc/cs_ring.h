@@ -361,8 +361,22 @@ struct RingLane {
             if (i >= 1 && k0 < sn) {
                 const uint32_t* row = (const uint32_t*)(stg + (k0 & ~3u));
                 const uint32_t sh = k0 & 3u, nd = (sn - k0) >> 2;
-                uint32_t cnt = 0, lo = row[0];
-                for (uint32_t d = 0; d < nd && i >= 1; d++) {
+                uint32_t cnt = 0, lo = row[0], d = 0;
+                // while i >= 4 a dword cannot take i below 1: every byte is live (no per-byte liveness or count)
+                for (; d < nd && i >= 4; d++) {
+                    const uint32_t hw = row[d + 1];
+                    const uint32_t x = __builtin_amdgcn_alignbyte(hw, lo, sh);
+                    lo = hw;
+#pragma unroll
+                    for (uint32_t t = 0; t < 4; t++) {
+                        const uint32_t u = __builtin_amdgcn_ubfe(x, 8 * t, 32u - __builtin_clz(i));
+                        const bool acc = u <= i;
+                        if (acc) put(hi - i, u);
+                        i -= acc ? 1u : 0u;
+                    }
+                    cnt += 4;
+                }
+                for (; d < nd && i >= 1; d++) {
                     const uint32_t hw = row[d + 1];
                     const uint32_t x = __builtin_amdgcn_alignbyte(hw, lo, sh);
                     lo = hw;
