@@ -249,8 +249,10 @@ struct Blackjack {
         uint8_t* deck = (uint8_t*)s;
         rng.draw_intervals(51u, [&](uint32_t k, uint32_t j) {
             const uint32_t i = 51u - k;
-            uint8_t* pi = deck + (i >> 2) * (WAVE * 4) + (i & 3u);
-            uint8_t* pj = deck + (j >> 2) * (WAVE * 4) + (j & 3u);
+            // (p >> 2) * 256 + (p & 3) as p + 252 * (p >> 2): a shift and a 24-bit multiply-add
+            static_assert(WAVE * 4 == 256, "deck byte address");
+            uint8_t* pi = deck + (i + __umul24(i >> 2, 252u));
+            uint8_t* pj = deck + (j + __umul24(j >> 2, 252u));
             const uint8_t ci = *pi, cj = *pj;
             *pi = cj;
             *pj = ci;
