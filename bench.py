@@ -225,13 +225,12 @@ def main():
     ap.add_argument('--no-precondition', dest='precondition', action='store_false',
                     help='time from freshly seeded streams (optimistic: no MT block refills yet)')
     ap.add_argument('--select', type=int, default=None,
-                    help='trajectory placement selection: allocate this many candidate trajectories and run on the '
-                         'fastest (1: off); default: what the library does, VecEnv.new_traj_out\'s '
-                         'PLACEMENT_CANDIDATES ranked by the placement probe; reported under "placement"')
-    ap.add_argument('--select-by', choices=('rollout', 'probe'), default='probe',
-                    help='how --select ranks its candidates: the placement probe before the preconditioning (default: '
-                         'the library\'s own choice, no env steps), or one untimed rollout launch per candidate after '
-                         'it (not what a library user gets)')
+                    help='trajectory placement selection: VecEnv.new_traj_out(select=...) allocates this many '
+                         'candidate trajectories and keeps the fastest (1: off); default: what the library does '
+                         '(PLACEMENT_CANDIDATES); reported under "placement"')
+    ap.add_argument('--select-by', choices=('rollout', 'probe'), default='rollout',
+                    help="new_traj_out's rank: 'rollout' (the library default: the probe's fast class, then one timed "
+                         "rollout launch each, env state saved and restored) or 'probe' (the placement probe alone)")
     ap.add_argument('--placement', type=int, default=3,
                     help='N=1: time a few launches into this many fresh trajectory allocations after the timed region '
                          '(untimed context under "placement"; 0: off)')
@@ -284,11 +283,10 @@ def main():
     N = args.envs or GAMES[game]['envs']
     env = ShardedVecEnv(game, N, rank, seed=42, device=local)   # global envs [rank*N, (rank+1)*N)
     env.reset()
-    by_rollout = (args.select or 0) > 1 and args.select_by == 'rollout'
-    cands = [env.new_traj_out(T, select=1) for _ in range(args.select)] if by_rollout else None
-    traj = cands[0] if by_rollout else env.new_traj_out(T, select=args.select)
-    probe_ms = list(getattr(env, 'placement_probe_ms', None) or []) if not by_rollout else []
-    select_ms = getattr(env, 'placement_select_ms', None) if not by_rollout else None
+    traj = env.new_traj_out(T, select=args.select, rank=args.select_by)   # the library's choice (DESIGN.md placement)
+    probe_ms = list(getattr(env, 'placement_probe_ms', None) or [])
+    trial_ms = getattr(env, 'placement_trial_ms', None)
+    select_ms = getattr(env, 'placement_select_ms', None)
 
     stream = torch.cuda.current_stream()
     t_launch = 0
@@ -297,25 +295,6 @@ def main():
         env.rollout(T, policy_seed=5, t0=t_launch * T, out=traj)
         t_launch += 1
     torch.cuda.synchronize()
-    cand_ms = None
-    if by_rollout:
-        # placement selection by the kernel itself (untimed, in steady state): two launches into each candidate
-        # trajectory allocation, interleaved; the timed region runs on the fastest, the others are freed
-        cand_ms = [[] for _ in cands]
-        for r in range(2):
-            for i, c in enumerate(cands):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                env.rollout(T, policy_seed=5, t0=t_launch * T, out=c)
-                e1.record(stream)
-                t_launch += 1
-                torch.cuda.synchronize()
-                cand_ms[i].append(e0.elapsed_time(e1))
-        best = min(range(len(cands)), key=lambda i: min(cand_ms[i]))
-        traj = cands[best]
-        cand_ms = [min(x) for x in cand_ms]
-        cands = None
-        torch.cuda.empty_cache()
     w0 = time.perf_counter()
     for w in range(args.warmup):
         env.rollout(T, policy_seed=5, t0=t_launch * T, out=traj)
@@ -510,20 +489,16 @@ def main():
                                   hip=state_snapshot.get('hip'), smi={k: smi.get(k) for k in keep},
                                   partition=(smi.get('partition') or {}).get('current_partition'),
                                   timed_window=power)
-        if placement is not None or probe_ms or cand_ms:
+        if placement is not None or probe_ms:
             line['placement'] = dict(placement or {})
-            if cand_ms:
-                line['placement']['selection'] = dict(
-                    candidates=len(cand_ms), by='rollout', rollout_ms=cand_ms,
-                    note='the timed trajectory is the fastest of the candidate allocations by one untimed rollout '
-                         'launch each (best of two, after the preconditioning; DESIGN 7)')
-            else:
-                line['placement']['selection'] = dict(
-                    candidates=len(probe_ms) or 1, by='probe', probe_ms=probe_ms or None,
-                    select_ms=select_ms, library_default=args.select is None,
-                    note='the timed trajectory is VecEnv.new_traj_out\'s choice: the fastest of the candidate '
-                         'allocations under the placement probe (cs_traj_probe: the rollout\'s writes, zeros, no game '
-                         'logic; DESIGN.md placement), chosen before warm-up -- what a library user gets')
+            line['placement']['selection'] = dict(
+                candidates=len(probe_ms) or 1, by=args.select_by, probe_ms=probe_ms or None, trial_ms=trial_ms,
+                select_ms=select_ms, library_default=args.select is None and args.select_by == 'rollout',
+                note='the timed trajectory is VecEnv.new_traj_out\'s choice, made before the preconditioning: '
+                     'candidate allocations probed (cs_traj_probe: the rollout\'s writes, zeros, no game logic), '
+                     'those in the fast class timed by one rollout launch each with the env state saved and restored '
+                     '(cs_state_save / cs_state_load), the fastest kept -- what a library user gets (DESIGN.md '
+                     'placement)')
         line.update(gather_info)
         if philox_info is not None:
             line['rng_philox'] = philox_info

@@ -67,10 +67,10 @@ typedef struct {
     int32_t envs_per_wave; /* envs one 64-lane wave of cs_rollout plays (doudizhu 2, heads-up Limit / No-limit 32,
                              otherwise 64): the write pattern cs_traj_probe reproduces */
 } cs_game_info;
-/* cs_game_info grows at its end between ABI versions (2: game_words, deal_queue_depth, envs_per_wave); a consumer
- * built against this header checks cs_abi_version() >= CS_ABI_VERSION before calling cs_game_info_get, which writes
- * sizeof(cs_game_info) bytes of this version. */
-#define CS_ABI_VERSION 2
+/* cs_game_info grows at its end between ABI versions (2: game_words, deal_queue_depth, envs_per_wave; 3 adds the
+ * cs_state_* functions); a consumer built against this header checks cs_abi_version() >= CS_ABI_VERSION before
+ * calling cs_game_info_get, which writes sizeof(cs_game_info) bytes of this version. */
+#define CS_ABI_VERSION 3
 
 /* Outputs of reset/step/observe, all device pointers, one row per env:
  *   obs    uint8  [n][obs_dim]     the current player's observation (values 0/1; blackjack: the two scores;
@@ -163,6 +163,16 @@ int cs_rollout(cs_handle* h, int32_t T, uint64_t policy_seed, uint64_t t0, uint6
  * this probe's time separates them exactly), so a caller can time it on a few candidate allocations and keep the
  * fastest (rlcard_amd.VecEnv.new_traj_out(select=k)). No reference counterpart (an allocation policy of this engine). */
 int cs_traj_probe(cs_handle* h, int32_t T, const cs_traj_out* out, void* stream);
+
+/* The whole engine state of a handle's envs -- MT streams, control words, game state, the rollout's staged stream rows
+ * -- as one device buffer of cs_state_bytes bytes: cs_state_save copies it out, cs_state_load back in (async on
+ * `stream`, device-to-device). A save / rollout / load sequence leaves the envs exactly as they were: how
+ * rlcard_amd.VecEnv.new_traj_out times a real rollout on each candidate trajectory allocation without moving the
+ * envs. The analogue of the reference's whole-game snapshot for step_back (rlcard/envs/env.py:88-106, the game's
+ * deepcopy history), for every env at once. Since ABI version 3. */
+int cs_state_bytes(const cs_handle* h, int64_t* bytes);
+int cs_state_save(cs_handle* h, void* buf, void* stream);
+int cs_state_load(cs_handle* h, const void* buf, void* stream);
 
 /* rlcard's reorganize (utils/utils.py:153-179: per player [state, action, reward, next_state, done]) and the DMC
  * return target (agents/dmc_agent/utils.py:97-163) of a cs_rollout trajectory of this handle, on the device. `traj`

@@ -29,7 +29,7 @@ class GameInfo(C.Structure):
                 ('deal_queue_depth', C.c_int32), ('envs_per_wave', C.c_int32)]
 
 
-ABI_VERSION = 2   # include/cardsim.h CS_ABI_VERSION: the cs_game_info layout above
+ABI_VERSION = 2   # the cs_game_info layout above: CS_ABI_VERSION 2 (3 keeps it and adds the cs_state_* functions)
 
 
 class StepOut(C.Structure):
@@ -59,7 +59,10 @@ SYMBOLS = ('cs_game_info_get', 'cs_create', 'cs_destroy', 'cs_seed', 'cs_reset',
            'cs_load_env_rng', 'cs_get_rng_ctl', 'cs_cfr_train', 'cs_debug_holdem_rank7', 'cs_debug_ddz_legal',
            'cs_debug_set_serial_refill', 'cs_debug_set_kernel_flags',
            'cs_dmc_create', 'cs_dmc_destroy', 'cs_dmc_fill', 'cs_dmc_gather', 'cs_dmc_status', 'cs_dmc_layer1',
-           'cs_dmc_select', 'cs_last_error', 'cs_version', 'cs_abi_version')
+           'cs_dmc_select', 'cs_last_error', 'cs_version', 'cs_abi_version', 'cs_state_bytes', 'cs_state_save',
+           'cs_state_load')
+# symbols an older library build may lack (A/B builds loaded with CARDSIM_LIB); callers check hasattr(lib(), name)
+OPTIONAL = ('cs_traj_probe', 'cs_state_bytes', 'cs_state_save', 'cs_state_load')
 
 _lib = None
 
@@ -88,6 +91,10 @@ def lib():
     L.cs_rollout.argtypes = [vp, i32, u64, u64, u64, C.POINTER(TrajOut), vp]
     if hasattr(L, 'cs_traj_probe'):   # (older A/B builds lack it)
         L.cs_traj_probe.argtypes = [vp, i32, C.POINTER(TrajOut), vp]
+    if hasattr(L, 'cs_state_bytes'):  # (ABI version 3)
+        L.cs_state_bytes.argtypes = [vp, vp]
+        L.cs_state_save.argtypes = [vp, vp, vp]
+        L.cs_state_load.argtypes = [vp, vp, vp]
     L.cs_transitions.argtypes = [vp, i32, C.POINTER(TrajOut), C.POINTER(TransOut), vp]
     L.cs_legal_lists.argtypes = [vp, vp, i64, vp, vp, vp, vp]
     L.cs_action_features.argtypes = [vp, vp, i64, vp, vp]
@@ -121,7 +128,7 @@ def lib():
                                                                                      ABI_VERSION))
     for name in SYMBOLS:
         if name not in ('cs_destroy', 'cs_dmc_destroy', 'cs_last_error', 'cs_version', 'cs_abi_version'):
-            if name == 'cs_traj_probe' and not hasattr(L, name):   # older A/B builds (CARDSIM_LIB) lack it
+            if name in OPTIONAL and not hasattr(L, name):   # older A/B builds (CARDSIM_LIB) lack it
                 continue
             getattr(L, name).restype = C.c_int
     _lib = L

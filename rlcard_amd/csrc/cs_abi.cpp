@@ -46,6 +46,29 @@ int set_device(const cs_handle* h)
     hipError_t e = hipSetDevice(h->device);
     return e == hipSuccess ? CS_OK : fail_hip(e, "hipSetDevice");
 }
+
+// u32 per env of the MT stream: doudizhu's two word blocks, the others' byte ring (info.rng_period bytes + wbuf)
+// (Blackjack shoes: one 624-word column per env, cs_blackjack_shoe.hip)
+size_t mt_words(const cs_game_info& info)
+{
+    return info.rng_period == 2 * 624 ? (size_t)(2 * 624)
+           : info.rng_period == 624   ? (size_t)624
+                                      : (size_t)cs::RING_ENV_WORDS_HOST;
+}
+
+// the device buffers that hold the envs' state (cs_state_*): pointer and bytes of each, in a fixed order
+int state_parts(const cs_handle* h, void* ptr[5], size_t bytes[5])
+{
+    const size_t n = (size_t)h->b.n;
+    const int64_t sb = cs::stage_bytes_per_env(h->b.game, h->info.num_players, h->b.num_decks);
+    ptr[0] = h->b.mt;    bytes[0] = n * mt_words(h->info) * sizeof(uint32_t);
+    ptr[1] = h->b.ctl;   bytes[1] = n * sizeof(uint32_t);
+    ptr[2] = h->b.state; bytes[2] = n * (size_t)h->info.state_words * sizeof(uint32_t);
+    ptr[3] = h->b.sctl;  bytes[3] = h->b.sctl ? n * sizeof(uint32_t) : 0;
+    ptr[4] = h->b.sbuf;  bytes[4] = h->b.sbuf ? (n + 63) / 64 * 64 * (size_t)sb : 0;
+    return 5;
+}
+size_t part_span(size_t bytes) { return (bytes + 255) / 256 * 256; }   // each part 256-B aligned in the buffer
 }  // namespace
 
 extern "C" {
@@ -97,11 +120,7 @@ int cs_create(cs_handle** out, int32_t game, int64_t num_envs, int32_t device, c
     h->b.table = nullptr;
     if ((r = set_device(h)) != CS_OK) { delete h; return r; }
     const size_t n = (size_t)num_envs;
-    // u32 per env of the MT stream: doudizhu's two word blocks, the others' byte ring (info.rng_period bytes + wbuf)
-    // (Blackjack shoes: one 624-word column per env, cs_blackjack_shoe.hip)
-    const size_t mtw = info.rng_period == 2 * 624 ? (size_t)(2 * 624)
-                       : info.rng_period == 624   ? (size_t)624
-                                                  : (size_t)cs::RING_ENV_WORDS_HOST;
+    const size_t mtw = mt_words(info);
     if ((e = hipMalloc((void**)&h->b.mt, n * mtw * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc((void**)&h->b.ctl, n * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc((void**)&h->b.state, n * (size_t)info.state_words * sizeof(uint32_t))) != hipSuccess) {
@@ -385,6 +404,41 @@ int cs_traj_probe(cs_handle* h, int32_t T, const cs_traj_out* out, void* stream)
                                          (hipStream_t)stream);
     return e == hipSuccess ? CS_OK : fail_hip(e, "cs_traj_probe");
 }
+
+int cs_state_bytes(const cs_handle* h, int64_t* bytes)
+{
+    if (!h || !bytes) return fail(CS_E_INVALID, "null argument");
+    void* ptr[5];
+    size_t nb[5];
+    size_t total = 0;
+    for (int i = 0, k = state_parts(h, ptr, nb); i < k; i++) total += part_span(nb[i]);
+    *bytes = (int64_t)total;
+    return CS_OK;
+}
+
+static int state_copy(cs_handle* h, void* buf, bool save, void* stream)
+{
+    if (!h || !buf) return fail(CS_E_INVALID, "null argument");
+    if (((uintptr_t)buf & 15u) != 0) return fail(CS_E_INVALID, "state buffer must be 16-byte aligned");
+    int r = set_device(h);
+    if (r != CS_OK) return r;
+    void* ptr[5];
+    size_t nb[5];
+    size_t off = 0;
+    for (int i = 0, k = state_parts(h, ptr, nb); i < k; i++) {
+        if (nb[i]) {
+            char* b = (char*)buf + off;
+            hipError_t e = save ? hipMemcpyAsync(b, ptr[i], nb[i], hipMemcpyDeviceToDevice, (hipStream_t)stream)
+                                : hipMemcpyAsync(ptr[i], b, nb[i], hipMemcpyDeviceToDevice, (hipStream_t)stream);
+            if (e != hipSuccess) return fail_hip(e, save ? "cs_state_save" : "cs_state_load");
+        }
+        off += part_span(nb[i]);
+    }
+    return CS_OK;
+}
+
+int cs_state_save(cs_handle* h, void* buf, void* stream) { return state_copy(h, buf, true, stream); }
+int cs_state_load(cs_handle* h, const void* buf, void* stream) { return state_copy(h, (void*)buf, false, stream); }
 
 int cs_transitions(cs_handle* h, int32_t T, const cs_traj_out* traj, const cs_trans_out* out, void* stream)
 {

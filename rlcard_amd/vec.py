@@ -137,7 +137,8 @@ class VecEnv:
 
     # trajectory candidates new_traj_out allocates and ranks by default (placement): where a trajectory lands
     # in HBM sets how fast the rollout can write it -- one allocation in three or so takes the rollout's writes 15-25 %
-    # slower, and the write-only probe tells those apart (not the few-% differences within a class)
+    # slower, which the write-only probe tells apart, and within the fast class a few % more that only the rollout
+    # itself shows
     PLACEMENT_CANDIDATES = 4
     FAST_CLASS = 0.93        # a candidate probing at >= this fraction of the best rate seen for its shape is "fast"
     _probe_best = {}         # (game, envs, T, final_obs) -> best probe rate (B/ms) seen in this process
@@ -150,14 +151,40 @@ class VecEnv:
             per += i.num_players * i.obs_dim
         return int(T) * self.num_envs * per
 
-    def new_traj_out(self, T, final_obs=False, select=None):
+    def state_bytes(self):
+        """bytes of the envs' whole engine state (include/cardsim.h cs_state_bytes), 0 on a library without it"""
+        L = _abi.lib()
+        if not hasattr(L, 'cs_state_bytes'):
+            return 0
+        n = C.c_int64()
+        _abi.check(L.cs_state_bytes(self._h, C.byref(n)), 'cs_state_bytes')
+        return n.value
+
+    def save_state(self, buf=None):
+        """the envs' whole engine state into a device buffer (cs_state_save; async on the env's stream) -> the buffer"""
+        if buf is None:
+            buf = torch.empty(self.state_bytes(), dtype=torch.uint8, device=self.device)
+        with torch.cuda.device(self.device):
+            _abi.check(_abi.lib().cs_state_save(self._h, _ptr(buf), self._stream()), 'cs_state_save')
+        return buf
+
+    def load_state(self, buf):
+        """the envs' whole engine state back from save_state's buffer (cs_state_load): rollouts, steps and resets
+        since the save are undone"""
+        with torch.cuda.device(self.device):
+            _abi.check(_abi.lib().cs_state_load(self._h, _ptr(buf), self._stream()), 'cs_state_load')
+
+    def new_traj_out(self, T, final_obs=False, select=None, rank='rollout'):
         """Trajectory buffers [T, N, ...] for rollout(). The placement is chosen: up to `select` candidates (default
         PLACEMENT_CANDIDATES, fewer when free device memory does not hold them all at once) are allocated side by
-        side, each is timed with the placement probe (probe_traj: the rollout's writes, zeros, no env state touched)
-        and the fastest is kept; the others go back to torch's caching allocator. On the default path the draw stops
-        early at a candidate probing in the fast class of the best rate this process has seen for the shape.
-        select=1: the first allocation, unprobed. The candidates' probe times are left in self.placement_probe_ms
-        (None when nothing was probed) and the time the choice took in self.placement_select_ms."""
+        side and each is timed with the placement probe (probe_traj: the rollout's writes, zeros, no env state
+        touched). rank='rollout' (the default): the candidates probing within FAST_CLASS of the best are then timed by
+        one rollout launch each (after one untimed launch) -- the envs' state saved before and loaded after
+        (save_state / load_state), so the envs end where they were -- and the fastest is kept; rank='probe': the fastest probe is kept, and on the
+        default path the draw stops early at a candidate probing in the fast class of the best rate this process has
+        seen for the shape. The others go back to torch's caching allocator. select=1: the first allocation,
+        untimed. Left in self: placement_probe_ms / placement_trial_ms (per candidate, None where not timed) and
+        placement_select_ms (the time the choice took)."""
         def one():
             o = self.new_step_out((T,))
             o['action'] = torch.empty((T, self.num_envs), dtype=self.action_dtype, device=self.device)
@@ -165,12 +192,18 @@ class VecEnv:
                 o['final_obs'] = torch.zeros((T, self.num_envs, self.num_players, self.obs_dim), dtype=torch.uint8,
                                              device=self.device)
             return o
+        if rank not in ('rollout', 'probe'):
+            raise ValueError("rank must be 'rollout' or 'probe'")
         k = self.PLACEMENT_CANDIDATES if select is None else int(select)
         nbytes = self.traj_bytes(T, final_obs)
+        sbytes = self.state_bytes() if rank == 'rollout' else 0
+        if rank == 'rollout' and sbytes == 0:
+            rank = 'probe'   # (a library without cs_state_*)
         if k > 1:
             free, _ = torch.cuda.mem_get_info(self.device)
-            k = min(k, int(0.9 * free) // max(1, nbytes))
+            k = min(k, (int(0.9 * free) - sbytes) // max(1, nbytes))
         self.placement_probe_ms = None
+        self.placement_trial_ms = None
         self.placement_select_ms = 0.0
         if k <= 1:
             return one()
@@ -182,13 +215,38 @@ class VecEnv:
             c = one()
             cands.append(c)
             times.append(min(self.probe_traj(c, T) for _ in range(2)))
-            if select is None and ref > 0 and nbytes / times[-1] >= self.FAST_CLASS * ref:
-                break   # (default path: a candidate in the shape's fast class ends the draw)
+            if rank == 'probe' and select is None and ref > 0 and nbytes / times[-1] >= self.FAST_CLASS * ref:
+                break   # (default probe path: a candidate in the shape's fast class ends the draw)
         VecEnv._probe_best[key] = max(ref, nbytes / min(times))
-        best = min(range(len(cands)), key=lambda i: times[i])
         self.placement_probe_ms = times
+        best, self.placement_trial_ms = self.rank_placements(cands, T, times, rank)
         self.placement_select_ms = (time.perf_counter() - t0) * 1e3
         return cands[best]
+
+    def rank_placements(self, cands, T, probe_ms, rank='rollout'):
+        """new_traj_out's choice among candidate trajectories with their probe times: rank='probe' the fastest
+        probe; rank='rollout' the candidates probing within FAST_CLASS of the best, timed by one rollout launch each
+        after one untimed launch, the envs' state saved before and loaded after. -> (index, trial ms per candidate
+        or None)"""
+        if rank == 'probe' or len(cands) == 1:
+            return min(range(len(cands)), key=lambda i: probe_ms[i]), None
+        fast = [i for i in range(len(cands)) if min(probe_ms) >= self.FAST_CLASS * probe_ms[i]]
+        trial = [None] * len(cands)
+        if len(fast) == 1:
+            return fast[0], trial
+        saved = self.save_state()
+        self.rollout(T, out=cands[fast[0]])
+        for i in fast:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.device(self.device):
+                e0.record()
+                self.rollout(T, out=cands[i])
+                e1.record()
+                e1.synchronize()
+            trial[i] = e0.elapsed_time(e1)
+        self.load_state(saved)
+        torch.cuda.current_stream(self.device).synchronize()
+        return min(fast, key=lambda i: trial[i]), trial
 
     def probe_traj(self, traj, T=None):
         """ms of one placement probe (include/cardsim.h cs_traj_probe: the rollout's writes, zeros, no state change)

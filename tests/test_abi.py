@@ -36,7 +36,7 @@ def test_game_info_shapes():
     for game, n in (('limit-holdem', 5), ('no-limit-holdem', 12), ('leduc-holdem', 4)):
         assert _abi.game_info(game, n)[0].envs_per_wave == 64
     assert _abi.game_info('blackjack', 6, 8)[0].envs_per_wave == 64
-    assert _abi.lib().cs_abi_version() == _abi.ABI_VERSION == 2
+    assert _abi.ABI_VERSION == 2 and _abi.lib().cs_abi_version() == 3   # 3: + cs_state_bytes / _save / _load
 
 
 def test_doudizhu_action_table_is_compiled_in():

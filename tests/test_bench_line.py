@@ -48,7 +48,9 @@ def test_bench_line_on_the_gpu():
     assert r['bound'] == 'hbm' and 0 < r['frac'] < 1.5 and r['kernel_ms_per_launch'] > 0
     wp = r['write_probe']
     assert wp['ms'] > 0 and wp['bytes'] > 0 and wp['kernel_over_probe'] > 0
-    sel = d['placement']['selection']   # the library's own choice (VecEnv.new_traj_out: probe-ranked candidates)
-    assert sel['by'] == 'probe' and sel['library_default'] and sel['candidates'] == len(sel['probe_ms']) >= 2
+    sel = d['placement']['selection']   # the library's own choice (VecEnv.new_traj_out: probe cut, rollout-ranked)
+    assert sel['by'] == 'rollout' and sel['library_default'] and sel['candidates'] == len(sel['probe_ms']) >= 2
     assert sel['select_ms'] > 0
+    trial = sel['trial_ms']
+    assert trial is None or (len(trial) == len(sel['probe_ms']) and any(t is not None and t > 0 for t in trial))
     assert len(d['placement']['kernel_ms_per_allocation']) == 2

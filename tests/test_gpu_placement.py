@@ -1,6 +1,7 @@
-"""The trajectory placement probe (include/cardsim.h cs_traj_probe) and VecEnv.new_traj_out(select=k): the probe
-writes zeros only inside the trajectory's tensors, leaves the envs untouched (a rollout after probing equals one
-without), and the selected trajectory is an ordinary one."""
+"""The trajectory placement probe (include/cardsim.h cs_traj_probe), the whole-state save / load (cs_state_*) and
+VecEnv.new_traj_out's choice: the probe writes zeros only inside the trajectory's tensors, a saved state loaded back
+undoes the rollouts since, the choice (probe cut, then one rollout launch per candidate with the state saved and
+restored) leaves the envs untouched, and it runs within 5 % of the fastest candidate."""
 import numpy as np
 import pytest
 import torch
@@ -43,13 +44,36 @@ def test_probe_writes_only_inside_the_tensors(game, n, T):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('game,n,T', GAMES)
+def test_state_save_load_undoes_rollouts(game, n, T):
+    v = VecEnv(game, n, seed=11, device=0)
+    v.reset()
+    tr = v.new_traj_out(T, select=1)
+    v.rollout(T, policy_seed=2, out=tr)
+    saved = v.save_state()
+    assert saved.numel() == v.state_bytes() > 0
+    first = {k: x.clone() for k, x in v.rollout(T, policy_seed=3, t0=T, out=tr).items()}
+    v.rollout(T, policy_seed=7, t0=2 * T, out=tr)   # moves the envs further
+    v.load_state(saved)
+    again = v.rollout(T, policy_seed=3, t0=T, out=tr)
+    torch.cuda.synchronize()
+    for key in first:
+        assert torch.equal(first[key], again[key]), (game, key)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('game,n,T', GAMES)
 def test_probe_and_selection_leave_the_envs_alone(game, n, T):
     a = VecEnv(game, n, seed=9, device=0)
     b = VecEnv(game, n, seed=9, device=0)
     a.reset()
     b.reset()
-    ta = a.new_traj_out(T)
-    tb = b.new_traj_out(T, select=3)
+    a.new_traj_out(T)   # the default path (probe cut; rollout-ranked when more than one candidate passes it)
+    assert a.placement_trial_ms is None or len(a.placement_trial_ms) == len(a.placement_probe_ms)
+    cands = [a.new_traj_out(T, select=1) for _ in range(3)]
+    pick, trial = a.rank_placements(cands, T, [1.0, 1.0, 1.0])   # all in the fast class: every one rolled out
+    assert all(x is not None and x > 0 for x in trial)
+    ta = cands[pick]
+    tb = b.new_traj_out(T, select=3, rank='probe')
     assert len(b.placement_probe_ms) == 3 and all(x > 0 for x in b.placement_probe_ms)
     b.probe_traj(tb, T)
     for k in range(2):
@@ -63,10 +87,10 @@ def test_probe_and_selection_leave_the_envs_alone(game, n, T):
 @pytest.mark.gpu
 @pytest.mark.parametrize('game,n,T', [('leduc-holdem', 1 << 20, 256), ('doudizhu', 65536, 64)])
 def test_default_placement_is_within_5pct_of_the_fastest(game, n, T):
-    """VecEnv.new_traj_out's default choice ranks candidate allocations by the write-only probe. Ground truth is the
-    rollout itself: four candidate trajectories (BASELINE shapes) alive at once, each timed by rollout launches in the
-    same process after a short warm-up; the allocation the probe ranks first must run within 5 % of the fastest
-    candidate (the probe separates the 20-25 % placement classes; within a class it cannot rank)."""
+    """VecEnv.new_traj_out's default ranking (rank_placements: the probe's fast class, then one rollout launch each).
+    Ground truth is the rollout itself: four candidate trajectories (BASELINE shapes) alive at once, each timed by three
+    rollout launches in the same process after a warm-up; the candidate the ranking picks must run within 5 % of the
+    fastest."""
     v = VecEnv(game, n, seed=42, device=0)
     v.reset()
     cands = [v.new_traj_out(T, select=1) for _ in range(4)]
@@ -75,6 +99,7 @@ def test_default_placement_is_within_5pct_of_the_fastest(game, n, T):
         v.rollout(T, 5, t * T, out=cands[t % 4])
         t += 1
     probe = [min(v.probe_traj(c, T) for _ in range(2)) for c in cands]
+    pick, trial = v.rank_placements(cands, T, probe)
     roll = [[] for _ in cands]
     for _ in range(3):
         for i, c in enumerate(cands):
@@ -86,5 +111,4 @@ def test_default_placement_is_within_5pct_of_the_fastest(game, n, T):
             torch.cuda.synchronize()
             roll[i].append(e0.elapsed_time(e1))
     best = [sorted(r)[1] for r in roll]
-    pick = min(range(len(cands)), key=lambda i: probe[i])
-    assert best[pick] <= 1.05 * min(best), (game, probe, best)
+    assert best[pick] <= 1.05 * min(best), (game, probe, trial, best)

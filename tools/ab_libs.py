@@ -50,7 +50,7 @@ for p in libs:
 allt = {p: [] for p in libs}
 for i in range(inst):
     use(libs[0])
-    tr = envs[libs[0]].new_traj_out(T, select=sel)   # one allocation, written by every library
+    tr = envs[libs[0]].new_traj_out(T, select=sel, rank='probe')   # one allocation, written by every library
     for p in libs:
         use(p)
         for _ in range(warm if i == 0 else 3):
