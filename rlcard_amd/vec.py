@@ -234,13 +234,15 @@ class VecEnv:
         trial = [None] * len(cands)
         if len(fast) == 1:
             return fast[0], trial
+        # (final_obs left out: the caller's rollouts only write its rows where a game ends, the others stay zero)
+        main = [{k: x for k, x in c.items() if k != 'final_obs'} for c in cands]
         saved = self.save_state()
-        self.rollout(T, out=cands[fast[0]])
+        self.rollout(T, out=main[fast[0]])
         for i in fast:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             with torch.cuda.device(self.device):
                 e0.record()
-                self.rollout(T, out=cands[i])
+                self.rollout(T, out=main[i])
                 e1.record()
                 e1.synchronize()
             trial[i] = e0.elapsed_time(e1)
