@@ -42,10 +42,18 @@ def test_probe_writes_only_inside_the_tensors(game, n, T):
     assert (b[inside] == 0).all(), 'the probe left part of a tensor unwritten'
 
 
+# the engine's other state layouts: N-player hold'em (no deal queue), Blackjack shoes (one MT column per env, no staged
+# rows), N-player Leduc, the Philox stream
+CONFIGS = [('limit-holdem', 300, 6, {'game_num_players': 5}), ('no-limit-holdem', 200, 6, {'game_num_players': 9}),
+           ('leduc-holdem', 300, 6, {'game_num_players': 4}), ('blackjack', 256, 5, {'game_num_players': 3,
+                                                                                     'game_num_decks': 4}),
+           ('blackjack', 256, 5, {'game_num_players': 6}), ('leduc-holdem', 500, 6, {'rng_mode': 'philox'})]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize('game,n,T', GAMES)
-def test_state_save_load_undoes_rollouts(game, n, T):
-    v = VecEnv(game, n, seed=11, device=0)
+@pytest.mark.parametrize('game,n,T,config', [g + (None,) for g in GAMES] + CONFIGS)
+def test_state_save_load_undoes_rollouts(game, n, T, config):
+    v = VecEnv(game, n, seed=11, device=0, config=config)
     v.reset()
     tr = v.new_traj_out(T, select=1)
     v.rollout(T, policy_seed=2, out=tr)
